@@ -1,0 +1,99 @@
+/* crc32c_batch.h -- batched CRC-32C on AMD Instinct MI355X (gfx950).
+ *
+ * New surface added next to crc32c.h.  Each entry point
+ * replaces a loop of scalar crc32c() calls in the reference:
+ *
+ *   crc32c_batch           N x crc32c(crc_in[i], base + off[i], len[i]):
+ *                          the spill CRC of storage.c:567 gathered per wbuf,
+ *                          the read-back CRC of storage.c:172 and
+ *                          proxy_internal.c:28 gathered per IO batch
+ *                          (extstore.c:853-945).
+ *   crc32c_verify_items    the read-verify compare of storage.c:159-178 applied
+ *                          to every item image of a packed extstore page
+ *                          (walk of storage.c:950-960): CRC over
+ *                          [off + 32, off + ITEM_ntotal) against the value
+ *                          stored in the item's exptime field (byte 28).
+ *   crc32c_batch_multi     crc32c_batch for host-resident batches split across
+ *                          several GPUs by bytes (no collective: items are
+ *                          independent).
+ *
+ * Results are bit-identical to the reference crc32c.c.  There is no CPU
+ * fallback: without a usable gfx950 device every batch entry point returns
+ * CRC32C_ENODEV.  Buffers stay owned by the caller and must stay valid until
+ * the call (or crc32c_batch_wait) returns.
+ */
+#ifndef CRC32C_BATCH_H
+#define CRC32C_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRC32C_OK 0
+#define CRC32C_ENODEV (-1) /* no gfx950 device visible */
+#define CRC32C_EHIP (-2)   /* HIP runtime error */
+#define CRC32C_EINVAL (-3) /* bad arguments */
+#define CRC32C_ENOMEM (-4) /* device or pinned allocation failed */
+
+/* flags */
+#define CRC32C_DEVICE 0x1u    /* every pointer in the batch is device memory of the
+                                 current HIP device */
+#define CRC32C_ASYNC 0x2u     /* with CRC32C_DEVICE: enqueue on `stream`, do not wait */
+#define CRC32C_ALIGNED16 0x4u /* caller guarantees every span start and length is a
+                                 multiple of 16 bytes (selects the aligned kernel) */
+
+/* A batch of byte spans inside one buffer.
+ *   span i = [base + (offsets ? offsets[i] : i * stride),  + (lens ? lens[i] : len))
+ *   out[i] = crc32c(crc_in ? crc_in[i] : 0, span i)
+ * base_bytes bounds every span (host batches copy [0, base_bytes) lazily). */
+typedef struct crc32c_spans {
+    const void *base;
+    uint64_t base_bytes;
+    const uint64_t *offsets;
+    uint64_t stride;
+    const uint32_t *lens;
+    uint32_t len;
+    const uint32_t *crc_in;
+    uint32_t *out;
+    uint64_t n;
+} crc32c_spans;
+
+/* Number of usable gfx950 devices (0 when none). */
+int crc32c_gpu_count(void);
+
+/* Checksum a batch.  Host batches are staged through pinned memory and the
+ * call returns when out[] is filled.  Device batches are enqueued on `stream`
+ * (a hipStream_t; NULL = the default stream) and, without CRC32C_ASYNC, the
+ * call returns when they are done. */
+int crc32c_batch(const crc32c_spans *spans, unsigned flags, void *stream);
+
+/* Host batch split across the first `ngpus` devices by bytes; one host thread
+ * per device, pinned H2D / D2H overlapped with the kernels. */
+int crc32c_batch_multi(const crc32c_spans *spans, int ngpus);
+
+/* Verify n item images of a packed page buffer (host or device per flags).
+ * ok[i] = 1 when item i's CRC matches its stored exptime; *nbad receives the
+ * number of mismatching (or malformed) items. */
+int crc32c_verify_items(const void *base, uint64_t base_bytes, const uint64_t *item_offsets,
+                        uint64_t n, uint8_t *ok, uint64_t *nbad, unsigned flags, void *stream);
+
+/* Asynchronous form of crc32c_batch for host batches: returns at once with a
+ * job handle; crc32c_batch_wait blocks until out[] is filled and frees it. */
+typedef struct crc32c_job *crc32c_job_t;
+int crc32c_batch_submit(const crc32c_spans *spans, unsigned flags, crc32c_job_t *job);
+int crc32c_batch_wait(crc32c_job_t job);
+
+const char *crc32c_strerror(int err);
+
+/* Duration of this thread's last synchronous device batch (milliseconds,
+ * hipEvent-measured on its stream); -1 before the first one. */
+float crc32c_last_kernel_ms(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CRC32C_BATCH_H */

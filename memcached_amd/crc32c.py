@@ -1,0 +1,138 @@
+"""Python face of the drop-in library, mirroring the reference interface.
+
+Scalar calls follow crc32c.h (reference crc32c.h:15-21): ``crc32c(crc, buf)``
+continues a CRC-32C over ``buf`` (first call with crc = 0, chaining allowed)
+and ``crc32c_sw`` is the table-driven variant.  Batch calls wrap
+include/crc32c_batch.h and run the gfx950 kernels:
+
+* ``batch``        out[i] = crc32c(crc_in[i] or 0, span i)  (storage.c:567, :172)
+* ``verify_items`` stored-CRC check of packed item images (storage.c:160-178)
+* ``batch_multi``  host batch split across GPUs by bytes
+
+Host inputs are numpy arrays (or bytes); device inputs are torch tensors on a
+HIP device, enqueued on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import CRC32C_ALIGNED16, CRC32C_ASYNC, CRC32C_DEVICE, Crc32cError, check, lib
+
+__all__ = ["crc32c", "crc32c_sw", "batch", "verify_items", "batch_multi", "gpu_count", "Crc32cError"]
+
+
+def _host_buf(data):
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        arr = np.frombuffer(data, dtype=np.uint8)
+    else:
+        arr = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return arr
+
+
+def crc32c(crc: int, data) -> int:
+    """crc32c(crc, buf, len) through the `crc32c` function-pointer symbol."""
+    arr = _host_buf(data)
+    return int(_lib.scalar_crc32c()(crc & 0xFFFFFFFF, arr.ctypes.data, arr.size))
+
+
+def crc32c_sw(crc: int, data) -> int:
+    arr = _host_buf(data)
+    return int(lib.crc32c_sw(crc & 0xFFFFFFFF, arr.ctypes.data, arr.size))
+
+
+def gpu_count() -> int:
+    return int(lib.crc32c_gpu_count())
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if _is_torch(x):
+        return x.data_ptr()
+    return x.ctypes.data
+
+
+def batch(buf, offsets=None, stride: int = 0, lens=None, length: int = 0, crc_in=None, out=None,
+          aligned16: bool = False, stream=None, asynchronous: bool = False):
+    """Batched CRC-32C of spans of ``buf``.
+
+    Span i = buf[off_i : off_i + len_i] with off_i = offsets[i] (or i*stride)
+    and len_i = lens[i] (or ``length``).  Host numpy inputs take the pinned
+    staging path; torch device tensors run in place on the current stream.
+    Returns ``out`` (uint32, one CRC per span).
+    """
+    dev = _is_torch(buf) and buf.is_cuda
+    if offsets is not None:
+        n = len(offsets)
+    elif lens is not None:
+        n = len(lens)
+    else:
+        raise ValueError("need offsets or lens to know the batch size")
+    if dev:
+        import torch
+        if out is None:
+            out = torch.empty(n, dtype=torch.int32, device=buf.device)
+        for t in (offsets, lens, crc_in):
+            if t is not None and not (_is_torch(t) and t.is_cuda and t.is_contiguous()):
+                raise ValueError("device batches need contiguous device tensors")
+        base_bytes = buf.numel() * buf.element_size()
+        if stream is None:
+            stream = torch.cuda.current_stream(buf.device).cuda_stream
+    else:
+        buf = _host_buf(buf)
+        base_bytes = buf.size
+        offsets = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint32)
+        crc_in = None if crc_in is None else np.ascontiguousarray(crc_in, dtype=np.uint32)
+        if out is None:
+            out = np.empty(n, dtype=np.uint32)
+    s = _lib.Spans(_ptr(buf), base_bytes, _ptr(offsets), stride, _ptr(lens), length, _ptr(crc_in),
+                   _ptr(out), n)
+    flags = (CRC32C_DEVICE if dev else 0) | (CRC32C_ALIGNED16 if aligned16 else 0)
+    if dev and asynchronous:
+        flags |= CRC32C_ASYNC
+    check(lib.crc32c_batch(ctypes.byref(s), flags, stream if dev else None), "crc32c_batch")
+    return out
+
+
+def batch_multi(buf, offsets=None, stride: int = 0, lens=None, length: int = 0, crc_in=None, ngpus: int = 0):
+    """Host batch split across ``ngpus`` devices (0 = all) by bytes."""
+    buf = _host_buf(buf)
+    offsets = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint32)
+    crc_in = None if crc_in is None else np.ascontiguousarray(crc_in, dtype=np.uint32)
+    n = len(offsets) if offsets is not None else len(lens)
+    out = np.empty(n, dtype=np.uint32)
+    s = _lib.Spans(_ptr(buf), buf.size, _ptr(offsets), stride, _ptr(lens), length, _ptr(crc_in),
+                   _ptr(out), n)
+    check(lib.crc32c_batch_multi(ctypes.byref(s), ngpus), "crc32c_batch_multi")
+    return out
+
+
+def verify_items(buf, item_offsets, stream=None):
+    """Verify packed item images; returns (ok uint8 array / tensor, nbad)."""
+    dev = _is_torch(buf) and buf.is_cuda
+    nbad = ctypes.c_uint64(0)
+    if dev:
+        import torch
+        n = item_offsets.numel()
+        ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(buf.device).cuda_stream
+        rc = lib.crc32c_verify_items(buf.data_ptr(), buf.numel() * buf.element_size(), item_offsets.data_ptr(),
+                                     n, ok.data_ptr(), ctypes.byref(nbad), CRC32C_DEVICE, stream)
+    else:
+        buf = _host_buf(buf)
+        offs = np.ascontiguousarray(item_offsets, dtype=np.uint64)
+        ok = np.empty(offs.size, dtype=np.uint8)
+        rc = lib.crc32c_verify_items(buf.ctypes.data, buf.size, offs.ctypes.data, offs.size, ok.ctypes.data,
+                                     ctypes.byref(nbad), 0, None)
+    check(rc, "crc32c_verify_items")
+    return ok, int(nbad.value)

@@ -1,0 +1,166 @@
+// crc32c_gf2.h -- host-side GF(2) operator algebra for CRC-32C (Castagnoli).
+//
+// The reference computes CRC-32C with a reflected register and the polynomial
+// 0x82f63b78 (crc32c.c:50).  Its hardware path merges three interleaved
+// streams with "zeros operators": 32x32 GF(2) matrices that advance a CRC
+// register over n zero bytes, applied through four byte-indexed tables
+// (crc32c.c:58-137).  This header is the build's own statement of that algebra;
+// it produces every constant table the HIP kernels and the host shim use:
+//
+//   Z            one zero byte:      r' = T0[r & 0xff] ^ (r >> 8)
+//   M_n = Z^n    n zero bytes;       M_n(r) = r * x^(8n) mod P
+//   raw(D)       register after D from a zero register (linear in D)
+//   crc32c(c, D) = ~( M_|D|(~c) ^ raw(D) )
+//
+// Everything here is plain integer arithmetic and runs once per table set.
+#pragma once
+
+#include <stdint.h>
+#include <string.h>
+
+namespace mcrc {
+
+constexpr uint32_t kPoly = 0x82f63b78u;  // reflected Castagnoli, crc32c.c:50
+
+// Register advanced by one zero bit: r * x mod P in the reflected basis.
+inline uint32_t zero_bit(uint32_t r) { return (r >> 1) ^ ((r & 1u) ? kPoly : 0u); }
+
+// Byte-wise Sarwate table: T0[b] = register after byte b from a zero register.
+inline void build_t0(uint32_t t0[256]) {
+    for (uint32_t b = 0; b < 256; ++b) {
+        uint32_t r = b;
+        for (int k = 0; k < 8; ++k) r = zero_bit(r);
+        t0[b] = r;
+    }
+}
+
+// A linear map on 32-bit CRC registers, stored by columns: col[i] = op(1 << i).
+struct Gf2Op {
+    uint32_t col[32];
+
+    uint32_t apply(uint32_t v) const {
+        uint32_t acc = 0;
+        for (int i = 0; v; ++i, v >>= 1)
+            if (v & 1u) acc ^= col[i];
+        return acc;
+    }
+    // (this o other)(v) = this(other(v))
+    Gf2Op after(const Gf2Op &other) const {
+        Gf2Op out;
+        for (int i = 0; i < 32; ++i) out.col[i] = apply(other.col[i]);
+        return out;
+    }
+    static Gf2Op identity() {
+        Gf2Op out;
+        for (int i = 0; i < 32; ++i) out.col[i] = 1u << i;
+        return out;
+    }
+    static Gf2Op one_zero_byte() {
+        Gf2Op out;
+        for (int i = 0; i < 32; ++i) {
+            uint32_t r = 1u << i;
+            for (int k = 0; k < 8; ++k) r = zero_bit(r);
+            out.col[i] = r;
+        }
+        return out;
+    }
+    // M_n: advance over n zero bytes (square-and-multiply over Z).
+    static Gf2Op zeros(uint64_t n) {
+        Gf2Op result = identity();
+        Gf2Op sq = one_zero_byte();
+        while (n) {
+            if (n & 1u) result = sq.after(result);
+            n >>= 1;
+            if (n) sq = sq.after(sq);
+        }
+        return result;
+    }
+    // Four byte-slice tables so that apply(v) = t[0][v&255] ^ t[1][(v>>8)&255]
+    // ^ t[2][(v>>16)&255] ^ t[3][v>>24]  (the form of crc32c.c:121-137).
+    void byte_tables(uint32_t t[4][256]) const {
+        for (int k = 0; k < 4; ++k)
+            for (uint32_t b = 0; b < 256; ++b) t[k][b] = apply(b << (8 * k));
+    }
+};
+
+// Reflected-basis polynomial product a(x) * b(x) mod P (bit 31 is x^0).
+inline uint32_t mulmodp(uint32_t a, uint32_t b) {
+    uint32_t prod = 0;
+    for (uint32_t m = 0x80000000u; m; m >>= 1) {
+        if (a & m) prod ^= b;
+        b = zero_bit(b);
+    }
+    return prod;
+}
+
+// x^(8n) mod P, reflected: multiplying a register by it advances n zero bytes.
+inline uint32_t xpow8n(uint64_t n) {
+    uint32_t result = 0x80000000u;  // x^0
+    uint32_t sq = 0x00800000u;      // x^8
+    while (n) {
+        if (n & 1u) result = mulmodp(result, sq);
+        n >>= 1;
+        if (n) sq = mulmodp(sq, sq);
+    }
+    return result;
+}
+
+// ---------------------------------------------------------------------------
+// LDS table images for the HIP kernels (layouts documented in crc32c_device.h).
+//   chunk = CH, bytes per lane per row.  Operator o = 0..6 fills aux tables
+//   4o..4o+3: o <= 5 is M_{chunk * 2^o}, o = 6 is M_{64 * chunk}.
+// ---------------------------------------------------------------------------
+constexpr int kImage1Dwords = 256 * 64;                    // SLICE 1: 64 KiB
+constexpr int kAux4Dwords = 28 * 256;                      // SLICE 4 aux: 28 KiB
+constexpr int kImage4Dwords = kAux4Dwords + 2 * 16384;     // SLICE 4: 156 KiB
+constexpr int kAuxTree = 0;
+constexpr int kAuxFold = 24;
+
+inline void aux_ops(uint32_t chunk, Gf2Op ops[7]) {
+    for (int k = 0; k < 6; ++k) ops[k] = Gf2Op::zeros((uint64_t)chunk << k);
+    ops[6] = Gf2Op::zeros((uint64_t)chunk * 64);
+}
+
+inline void build_lds_image1(uint32_t *img, uint32_t chunk) {
+    memset(img, 0, sizeof(uint32_t) * kImage1Dwords);
+    uint32_t t0[256];
+    build_t0(t0);
+    for (int e = 0; e < 256; ++e)
+        for (int l = 0; l < 32; ++l) img[e * 64 + l] = t0[e];
+    Gf2Op ops[7];
+    aux_ops(chunk, ops);
+    for (int o = 0; o < 7; ++o) {
+        uint32_t tabs[4][256];
+        ops[o].byte_tables(tabs);
+        for (int k = 0; k < 4; ++k) {
+            const int t = 4 * o + k;
+            for (uint32_t e = 0; e < 256; ++e) img[(8 * t + (e >> 5)) * 64 + 32 + (e & 31)] = tabs[k][e];
+        }
+    }
+}
+
+inline void build_lds_image4(uint32_t *img, uint32_t chunk) {
+    memset(img, 0, sizeof(uint32_t) * kImage4Dwords);
+    Gf2Op ops[7];
+    aux_ops(chunk, ops);
+    for (int o = 0; o < 7; ++o) {
+        uint32_t tabs[4][256];
+        ops[o].byte_tables(tabs);
+        for (int k = 0; k < 4; ++k)
+            for (uint32_t e = 0; e < 256; ++e) img[(4 * o + k) * 256 + e] = tabs[k][e];
+    }
+    uint32_t t[4][256];  // t[k][b]: byte b then k zero bytes
+    build_t0(t[0]);
+    for (int k = 1; k < 4; ++k)
+        for (int b = 0; b < 256; ++b) t[k][b] = t[0][t[k - 1][b] & 0xffu] ^ (t[k - 1][b] >> 8);
+    uint32_t *set_a = img + kAux4Dwords, *set_b = set_a + 16384;
+    for (int e = 0; e < 256; ++e)
+        for (int l = 0; l < 32; ++l) {
+            set_a[e * 64 + l] = t[3][e];
+            set_a[e * 64 + 32 + l] = t[2][e];
+            set_b[e * 64 + l] = t[1][e];
+            set_b[e * 64 + 32 + l] = t[0][e];
+        }
+}
+
+}  // namespace mcrc

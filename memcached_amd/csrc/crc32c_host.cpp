@@ -1,0 +1,129 @@
+// crc32c_host.cpp -- host CRC-32C used by the scalar drop-in symbol.
+#include "crc32c_host.h"
+
+#include <mutex>
+
+#include "crc32c_gf2.h"
+
+#if defined(__x86_64__)
+#include <cpuid.h>
+#include <nmmintrin.h>
+#endif
+
+namespace mcrc {
+
+namespace {
+
+std::once_flag g_once;
+uint32_t g_slice[8][256];           // g_slice[k][b]: byte b followed by k zero bytes
+constexpr size_t kStreamBlock = 4096;  // bytes per stream per round of the 3-way loop
+uint32_t g_shift_block[4][256];     // M_{kStreamBlock}
+uint32_t g_shift_small[4][256];     // M_{kSmallBlock}
+constexpr size_t kSmallBlock = 256;
+
+void build_all() {
+    build_t0(g_slice[0]);
+    for (int k = 1; k < 8; ++k)
+        for (int b = 0; b < 256; ++b) {
+            const uint32_t prev = g_slice[k - 1][b];
+            g_slice[k][b] = g_slice[0][prev & 0xffu] ^ (prev >> 8);
+        }
+    Gf2Op::zeros(kStreamBlock).byte_tables(g_shift_block);
+    Gf2Op::zeros(kSmallBlock).byte_tables(g_shift_small);
+}
+
+inline uint32_t apply4(const uint32_t t[4][256], uint32_t v) {
+    return t[0][v & 0xffu] ^ t[1][(v >> 8) & 0xffu] ^ t[2][(v >> 16) & 0xffu] ^ t[3][v >> 24];
+}
+
+inline uint64_t load64(const unsigned char *p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+
+// Register-level slice-by-8 (no pre/post inversion).
+uint32_t reg_sw(uint32_t r, const unsigned char *p, size_t n) {
+    while (n && ((uintptr_t)p & 7u)) {
+        r = g_slice[0][(r ^ *p++) & 0xffu] ^ (r >> 8);
+        --n;
+    }
+    for (; n >= 8; n -= 8, p += 8) {
+        const uint64_t x = load64(p) ^ r;
+        r = g_slice[7][x & 0xffu] ^ g_slice[6][(x >> 8) & 0xffu] ^ g_slice[5][(x >> 16) & 0xffu] ^
+            g_slice[4][(x >> 24) & 0xffu] ^ g_slice[3][(x >> 32) & 0xffu] ^
+            g_slice[2][(x >> 40) & 0xffu] ^ g_slice[1][(x >> 48) & 0xffu] ^ g_slice[0][x >> 56];
+    }
+    while (n--) r = g_slice[0][(r ^ *p++) & 0xffu] ^ (r >> 8);
+    return r;
+}
+
+#if defined(__x86_64__)
+// Three streams of `blk` bytes per round: the crc32 instruction has a latency of
+// three and a throughput of one, so three independent chains keep it busy.
+__attribute__((target("sse4.2"))) uint64_t three_way(uint64_t r, const unsigned char *&p, size_t &n,
+                                                     size_t blk, const uint32_t (*shift)[256]) {
+    while (n >= 3 * blk) {
+        uint64_t a = r, b = 0, c = 0;
+        const unsigned char *pa = p, *pb = p + blk, *pc = p + 2 * blk;
+        for (size_t i = 0; i < blk; i += 8) {
+            a = _mm_crc32_u64(a, load64(pa + i));
+            b = _mm_crc32_u64(b, load64(pb + i));
+            c = _mm_crc32_u64(c, load64(pc + i));
+        }
+        r = apply4(shift, apply4(shift, (uint32_t)a) ^ (uint32_t)b) ^ (uint32_t)c;
+        p += 3 * blk;
+        n -= 3 * blk;
+    }
+    return r;
+}
+
+__attribute__((target("sse4.2"))) uint32_t reg_hw(uint32_t r32, const unsigned char *p, size_t n) {
+    uint64_t r = r32;
+    while (n && ((uintptr_t)p & 7u)) {
+        r = _mm_crc32_u8((uint32_t)r, *p++);
+        --n;
+    }
+    r = three_way(r, p, n, kStreamBlock, g_shift_block);
+    r = three_way(r, p, n, kSmallBlock, g_shift_small);
+    for (; n >= 8; n -= 8, p += 8) r = _mm_crc32_u64(r, load64(p));
+    while (n--) r = _mm_crc32_u8((uint32_t)r, *p++);
+    return (uint32_t)r;
+}
+#endif
+
+}  // namespace
+
+void host_tables_init() { std::call_once(g_once, build_all); }
+
+bool host_has_sse42() {
+#if defined(__x86_64__)
+    unsigned eax, ebx, ecx, edx;
+    if (!__get_cpuid(1, &eax, &ebx, &ecx, &edx)) return false;
+    return (ecx >> 20) & 1u;
+#else
+    return false;
+#endif
+}
+
+uint32_t crc32c_host_sw(uint32_t crc, const void *buf, size_t len) {
+    host_tables_init();
+    return ~reg_sw(~crc, static_cast<const unsigned char *>(buf), len);
+}
+
+uint32_t crc32c_host_hw(uint32_t crc, const void *buf, size_t len) {
+    host_tables_init();
+#if defined(__x86_64__)
+    return ~reg_hw(~crc, static_cast<const unsigned char *>(buf), len);
+#else
+    return ~reg_sw(~crc, static_cast<const unsigned char *>(buf), len);
+#endif
+}
+
+uint32_t crc32c_host_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+    // crc(A||B) = ~(M_|B|(~crc(A)) ^ raw(B)), raw(B) = ~crc_b ^ M_|B|(~0)
+    // => crc(A||B) = M_|B|(crc_a) ^ crc_b   (the ~ terms cancel by linearity)
+    return mulmodp(crc_a, xpow8n(len_b)) ^ crc_b;
+}
+
+}  // namespace mcrc

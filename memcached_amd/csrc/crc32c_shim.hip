@@ -1,0 +1,525 @@
+// crc32c_shim.hip -- the C-ABI library (libmcrc32c.so): memcached's crc32c.h
+// surface plus the batched gfx950 entry points of crc32c_batch.h.
+//
+// Host side of the drop-in boundary.  The scalar symbols replace crc32c.c
+// (crc32c.c:47, :266-275, :507-513); the batch symbols replace loops of those
+// calls in storage.c / proxy_internal.c (see include/crc32c_batch.h).
+#include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/crc32c.h"
+#include "../../include/crc32c_batch.h"
+#include "crc32c_gf2.h"
+#include "crc32c_host.h"
+#include "crc32c_kernels.hip"
+
+// ---------------------------------------------------------------------------
+// Scalar drop-in (crc32c.h)
+// ---------------------------------------------------------------------------
+extern "C" {
+
+crc_func crc32c = nullptr;
+
+void crc32c_init(void) {
+    mcrc::host_tables_init();
+    crc32c = mcrc::host_has_sse42() ? mcrc::crc32c_host_hw : mcrc::crc32c_host_sw;
+}
+
+uint32_t crc32c_sw(uint32_t crc, void const *buf, size_t len) { return mcrc::crc32c_host_sw(crc, buf, len); }
+
+uint32_t crc32c_sw_little(uint32_t crc, void const *buf, size_t len) {
+    return mcrc::crc32c_host_sw(crc, buf, len);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Per-device state
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int kBlock = 1024;                    // 16 waves, 32 lane groups
+constexpr uint32_t kItemsPerBlockStep = 32;     // one span per 32-lane group
+constexpr uint32_t kFixedLen = 4096;            // K1 instance: 2 rows x 32 lanes x 64 B
+
+thread_local float g_last_kernel_ms = -1.0f;
+
+struct Device {
+    int id = -1;
+    int cus = 0;
+    bool ok = false;
+    uint4 *img = nullptr;       // LDS table image (CH = 64)
+    uint32_t *xpow = nullptr;   // 3 x 1024 x^(8n) table
+    uint4 *zero = nullptr;      // 16 zero bytes
+    unsigned long long *nbad = nullptr;
+    hipStream_t stream = nullptr, copy = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::mutex mu;              // serialises host batches on this device
+    // host-batch staging: two device slots + two pinned slots
+    uint8_t *dbuf[2] = {nullptr, nullptr};
+    uint8_t *pin[2] = {nullptr, nullptr};
+    uint64_t slot_bytes = 0;
+    uint64_t *doffs[2] = {nullptr, nullptr};
+    uint32_t *dlens[2] = {nullptr, nullptr}, *dcin[2] = {nullptr, nullptr}, *dout[2] = {nullptr, nullptr};
+    uint64_t *hoffs[2] = {nullptr, nullptr};  // pinned twins of the descriptor slots
+    uint32_t *hlens[2] = {nullptr, nullptr}, *hcin[2] = {nullptr, nullptr}, *hout[2] = {nullptr, nullptr};
+    uint64_t slot_items = 0;
+};
+
+std::mutex g_dev_mu;
+std::vector<std::unique_ptr<Device>> g_devs;
+int g_ndev = -1;
+
+#define HIP_OK(x)                              \
+    do {                                       \
+        if ((x) != hipSuccess) return CRC32C_EHIP; \
+    } while (0)
+
+int count_gfx950() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int good = 0;
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, d) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ++good;
+    }
+    return good == n ? n : good;  // assume homogeneous nodes
+}
+
+int init_device(Device &d, int id) {
+    d.id = id;
+    HIP_OK(hipSetDevice(id));
+    hipDeviceProp_t p;
+    HIP_OK(hipGetDeviceProperties(&p, id));
+    if (strncmp(p.gcnArchName, "gfx950", 6) != 0) return CRC32C_ENODEV;
+    d.cus = p.multiProcessorCount;
+    std::vector<uint32_t> img(mcrc::kImage4Dwords);
+    mcrc::build_lds_image4(img.data(), mcrc_dev::kSpanCH);
+    std::vector<uint32_t> xp(3 * 1024);
+    for (uint32_t j = 0; j < 1024; ++j) {
+        xp[j] = mcrc::xpow8n(j);
+        xp[1024 + j] = mcrc::xpow8n((uint64_t)j << 10);
+        xp[2048 + j] = mcrc::xpow8n((uint64_t)j << 20);
+    }
+    HIP_OK(hipMalloc(&d.img, img.size() * 4));
+    HIP_OK(hipMemcpy(d.img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMalloc(&d.xpow, xp.size() * 4));
+    HIP_OK(hipMemcpy(d.xpow, xp.data(), xp.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMalloc(&d.zero, 64));
+    HIP_OK(hipMemset(d.zero, 0, 64));
+    HIP_OK(hipMalloc(&d.nbad, sizeof(unsigned long long)));
+    HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&d.ev0));
+    HIP_OK(hipEventCreate(&d.ev1));
+    const void *kernels[] = {
+        (const void *)mcrc_dev::k_fixed<4, 32, 64, 2, 0>,  (const void *)mcrc_dev::k_spans<false, 0>,
+        (const void *)mcrc_dev::k_spans<true, 0>,           (const void *)mcrc_dev::k_spans<true, 1>,
+    };
+    for (const void *k : kernels)
+        HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImage4Bytes));
+    d.ok = true;
+    return CRC32C_OK;
+}
+
+// Device state for the calling thread's current HIP device.
+int current_device(Device **out) {
+    int id = 0;
+    if (hipGetDevice(&id) != hipSuccess) return CRC32C_ENODEV;
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (g_ndev < 0) {
+        g_ndev = count_gfx950();
+        for (int i = 0; i < g_ndev; ++i) g_devs.emplace_back(new Device());
+    }
+    if (id < 0 || id >= g_ndev) return CRC32C_ENODEV;
+    Device &d = *g_devs[id];
+    if (!d.ok) {
+        const int rc = init_device(d, id);
+        if (rc != CRC32C_OK) return rc;
+    }
+    *out = &d;
+    return CRC32C_OK;
+}
+
+int grid_for(const Device &d, uint64_t n) {
+    const uint64_t want = (n + kItemsPerBlockStep - 1) / kItemsPerBlockStep;
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)d.cus));
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Enqueue the kernel for a device-resident batch on `st`.
+int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t st) {
+    if (s.n == 0) return CRC32C_OK;
+    const bool fixed = s.offsets == nullptr && s.lens == nullptr;
+    const uint32_t kspan = fixed ? mcrc::xpow8n(s.len) : 0u;
+    if (fixed && s.len == kFixedLen && aligned16(s.base) && (s.stride & 15u) == 0) {
+        const uint32_t kfinal = ~mcrc::Gf2Op::zeros(s.len).apply(0xffffffffu);
+        hipLaunchKernelGGL((mcrc_dev::k_fixed<4, 32, 64, 2, 0>), dim3(grid_for(d, s.n)), dim3(kBlock),
+                           mcrc_dev::kLdsImage4Bytes, st, (const uint8_t *)s.base, s.stride, s.n,
+                           d.img, kfinal, kspan, s.crc_in, s.out);
+    } else {
+        mcrc_dev::SpanArgs a{};
+        a.base = (const uint8_t *)s.base;
+        a.base_bytes = s.base_bytes;
+        a.offsets = s.offsets;
+        a.stride = s.stride;
+        a.lens = s.lens;
+        a.len = s.len;
+        a.kspan = kspan;
+        a.crc_in = s.crc_in;
+        a.out = s.out;
+        a.n = s.n;
+        a.xpow = d.xpow;
+        a.zero = d.zero;
+        const bool aligned = (flags & CRC32C_ALIGNED16) ||
+                             (fixed && aligned16(s.base) && (s.stride & 15u) == 0 && (s.len & 15u) == 0);
+        if (aligned)
+            hipLaunchKernelGGL((mcrc_dev::k_spans<false, 0>), dim3(grid_for(d, s.n)), dim3(kBlock),
+                               mcrc_dev::kLdsImage4Bytes, st, a, d.img);
+        else
+            hipLaunchKernelGGL((mcrc_dev::k_spans<true, 0>), dim3(grid_for(d, s.n)), dim3(kBlock),
+                               mcrc_dev::kLdsImage4Bytes, st, a, d.img);
+    }
+    return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
+}
+
+bool is_pinned_or_device(const void *p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost || at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+uint64_t span_off(const crc32c_spans &s, uint64_t i) { return s.offsets ? s.offsets[i] : i * s.stride; }
+uint64_t span_len(const crc32c_spans &s, uint64_t i) { return s.lens ? s.lens[i] : s.len; }
+
+int ensure_slots(Device &d, uint64_t bytes, uint64_t items) {
+    if (d.slot_bytes < bytes) {
+        for (int k = 0; k < 2; ++k) {
+            if (d.dbuf[k]) (void)hipFree(d.dbuf[k]);
+            if (d.pin[k]) (void)hipHostFree(d.pin[k]);
+            d.dbuf[k] = nullptr;
+            d.pin[k] = nullptr;
+            if (hipMalloc(&d.dbuf[k], bytes) != hipSuccess) return CRC32C_ENOMEM;
+            if (hipHostMalloc(&d.pin[k], bytes, hipHostMallocDefault) != hipSuccess) return CRC32C_ENOMEM;
+        }
+        d.slot_bytes = bytes;
+    }
+    if (d.slot_items < items) {
+        for (int k = 0; k < 2; ++k) {
+            (void)hipFree(d.doffs[k]);
+            (void)hipFree(d.dlens[k]);
+            (void)hipFree(d.dcin[k]);
+            (void)hipFree(d.dout[k]);
+            (void)hipHostFree(d.hoffs[k]);
+            (void)hipHostFree(d.hlens[k]);
+            (void)hipHostFree(d.hcin[k]);
+            (void)hipHostFree(d.hout[k]);
+            if (hipMalloc(&d.doffs[k], items * 8) != hipSuccess || hipMalloc(&d.dlens[k], items * 4) != hipSuccess ||
+                hipMalloc(&d.dcin[k], items * 4) != hipSuccess || hipMalloc(&d.dout[k], items * 4) != hipSuccess ||
+                hipHostMalloc(&d.hoffs[k], items * 8, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc(&d.hlens[k], items * 4, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc(&d.hcin[k], items * 4, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc(&d.hout[k], items * 4, hipHostMallocDefault) != hipSuccess)
+                return CRC32C_ENOMEM;
+        }
+        d.slot_items = items;
+    }
+    return CRC32C_OK;
+}
+
+constexpr uint64_t kSlotBytes = 256ull << 20;  // bytes of span data per pipeline stage
+constexpr uint64_t kSlotItems = 1ull << 20;
+
+// Host-resident batch on one device.  Chunks of consecutive spans (offsets
+// must be non-decreasing) go through two pipeline slots: while chunk c is
+// checksummed, chunk c+1 is staged into pinned memory (unless the caller's
+// buffer is already pinned) and copied H2D on the copy stream.  Descriptors and
+// results travel through pinned twins so no copy touches pageable memory.
+int run_host_batch(Device &d, const crc32c_spans &s) {
+    std::lock_guard<std::mutex> lk(d.mu);
+    HIP_OK(hipSetDevice(d.id));
+    if (s.n == 0) return CRC32C_OK;
+    for (uint64_t i = 1; i < s.n; ++i)
+        if (span_off(s, i) < span_off(s, i - 1)) return CRC32C_EINVAL;
+    for (uint64_t i = 0; i < s.n; ++i)
+        if (span_off(s, i) + span_len(s, i) > s.base_bytes || span_len(s, i) > kSlotBytes - 16)
+            return CRC32C_EINVAL;
+    int rc = ensure_slots(d, kSlotBytes, kSlotItems);
+    if (rc) return rc;
+    const bool src_pinned = is_pinned_or_device(s.base);
+    const uint8_t *src = (const uint8_t *)s.base;
+    hipEvent_t copied[2], done[2];
+    for (int k = 0; k < 2; ++k) {
+        HIP_OK(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
+    }
+    uint64_t pend_i0[2] = {0, 0}, pend_n[2] = {0, 0};  // results waiting in hout[slot]
+    auto drain = [&](int k) -> int {
+        if (!pend_n[k]) return CRC32C_OK;
+        HIP_OK(hipEventSynchronize(done[k]));
+        memcpy(s.out + pend_i0[k], d.hout[k], pend_n[k] * 4);
+        pend_n[k] = 0;
+        return CRC32C_OK;
+    };
+    uint64_t i0 = 0;
+    int slot = 0;
+    while (i0 < s.n) {
+        const uint64_t lo = span_off(s, i0) & ~15ull;
+        uint64_t i1 = i0, hi = lo;
+        while (i1 < s.n && i1 - i0 < kSlotItems) {
+            const uint64_t e = span_off(s, i1) + span_len(s, i1);
+            if (std::max(hi, e) - lo > kSlotBytes) break;
+            hi = std::max(hi, e);
+            ++i1;
+        }
+        const uint64_t bytes = hi - lo, cnt = i1 - i0;
+        if ((rc = drain(slot))) return rc;  // slot free: its kernel and D2H are done
+        const uint8_t *h2d_src = src + lo;
+        if (!src_pinned) {
+            memcpy(d.pin[slot], src + lo, bytes);
+            h2d_src = d.pin[slot];
+        }
+        for (uint64_t i = 0; i < cnt; ++i) d.hoffs[slot][i] = span_off(s, i0 + i) - lo;
+        if (s.lens) memcpy(d.hlens[slot], s.lens + i0, cnt * 4);
+        if (s.crc_in) memcpy(d.hcin[slot], s.crc_in + i0, cnt * 4);
+        HIP_OK(hipMemcpyAsync(d.dbuf[slot], h2d_src, bytes, hipMemcpyHostToDevice, d.copy));
+        HIP_OK(hipMemcpyAsync(d.doffs[slot], d.hoffs[slot], cnt * 8, hipMemcpyHostToDevice, d.copy));
+        if (s.lens) HIP_OK(hipMemcpyAsync(d.dlens[slot], d.hlens[slot], cnt * 4, hipMemcpyHostToDevice, d.copy));
+        if (s.crc_in) HIP_OK(hipMemcpyAsync(d.dcin[slot], d.hcin[slot], cnt * 4, hipMemcpyHostToDevice, d.copy));
+        HIP_OK(hipEventRecord(copied[slot], d.copy));
+        HIP_OK(hipStreamWaitEvent(d.stream, copied[slot], 0));
+        crc32c_spans sub{};
+        sub.base = d.dbuf[slot];
+        sub.base_bytes = bytes;
+        sub.offsets = d.doffs[slot];
+        sub.lens = s.lens ? d.dlens[slot] : nullptr;
+        sub.len = s.len;
+        sub.crc_in = s.crc_in ? d.dcin[slot] : nullptr;
+        sub.out = d.dout[slot];
+        sub.n = cnt;
+        if ((rc = enqueue_device(d, sub, 0, d.stream))) return rc;
+        HIP_OK(hipMemcpyAsync(d.hout[slot], d.dout[slot], cnt * 4, hipMemcpyDeviceToHost, d.stream));
+        HIP_OK(hipEventRecord(done[slot], d.stream));
+        pend_i0[slot] = i0;
+        pend_n[slot] = cnt;
+        i0 = i1;
+        slot ^= 1;
+    }
+    if ((rc = drain(slot)) || (rc = drain(slot ^ 1))) return rc;
+    for (int k = 0; k < 2; ++k) {
+        (void)hipEventDestroy(copied[k]);
+        (void)hipEventDestroy(done[k]);
+    }
+    return CRC32C_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Batch C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int crc32c_gpu_count(void) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (g_ndev < 0) {
+        g_ndev = count_gfx950();
+        for (int i = 0; i < g_ndev; ++i) g_devs.emplace_back(new Device());
+    }
+    return g_ndev;
+}
+
+const char *crc32c_strerror(int err) {
+    switch (err) {
+        case CRC32C_OK: return "ok";
+        case CRC32C_ENODEV: return "no gfx950 device";
+        case CRC32C_EHIP: return "HIP runtime error";
+        case CRC32C_EINVAL: return "invalid argument";
+        case CRC32C_ENOMEM: return "out of device or pinned memory";
+        default: return "unknown error";
+    }
+}
+
+float crc32c_last_kernel_ms(void) { return g_last_kernel_ms; }
+
+int crc32c_batch(const crc32c_spans *s, unsigned flags, void *stream) {
+    if (!s || (s->n && (!s->base || !s->out))) return CRC32C_EINVAL;
+    Device *d = nullptr;
+    int rc = current_device(&d);
+    if (rc) return rc;
+    if (!(flags & CRC32C_DEVICE)) return run_host_batch(*d, *s);
+    // Device batches run on the caller's stream; NULL is the default stream, so
+    // the kernel is ordered after whatever produced the buffers there.
+    hipStream_t st = (hipStream_t)stream;
+    const bool timed = !(flags & CRC32C_ASYNC);
+    if (timed) HIP_OK(hipEventRecord(d->ev0, st));
+    rc = enqueue_device(*d, *s, flags, st);
+    if (rc) return rc;
+    if (!timed) return CRC32C_OK;
+    HIP_OK(hipEventRecord(d->ev1, st));
+    HIP_OK(hipEventSynchronize(d->ev1));
+    (void)hipEventElapsedTime(&g_last_kernel_ms, d->ev0, d->ev1);
+    return CRC32C_OK;
+}
+
+int crc32c_verify_items(const void *base, uint64_t base_bytes, const uint64_t *item_offsets, uint64_t n,
+                        uint8_t *ok, uint64_t *nbad, unsigned flags, void *stream) {
+    if (!base || !item_offsets || !ok || !nbad) return CRC32C_EINVAL;
+    Device *d = nullptr;
+    int rc = current_device(&d);
+    if (rc) return rc;
+    if (n == 0) {
+        *nbad = 0;
+        return CRC32C_OK;
+    }
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t st = (hipStream_t)stream;  // NULL: the default stream
+    const bool dev = flags & CRC32C_DEVICE;
+    const uint8_t *dbase = (const uint8_t *)base;
+    const uint64_t *doffs = item_offsets;
+    uint8_t *dok = ok;
+    std::vector<void *> tmp;
+    auto dalloc = [&](size_t bytes) -> void * {
+        void *p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        tmp.push_back(p);
+        return p;
+    };
+    auto cleanup = [&]() {
+        for (void *p : tmp) (void)hipFree(p);
+    };
+    if (!dev) {
+        uint8_t *b = (uint8_t *)dalloc(base_bytes);
+        uint64_t *o = (uint64_t *)dalloc(n * 8);
+        dok = (uint8_t *)dalloc(n);
+        if (!b || !o || !dok) {
+            cleanup();
+            return CRC32C_ENOMEM;
+        }
+        if (hipMemcpyAsync(b, base, base_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(o, item_offsets, n * 8, hipMemcpyHostToDevice, st) != hipSuccess) {
+            cleanup();
+            return CRC32C_EHIP;
+        }
+        dbase = b;
+        doffs = o;
+    }
+    mcrc_dev::SpanArgs a{};
+    a.base = dbase;
+    a.base_bytes = base_bytes;
+    a.offsets = doffs;
+    a.ok = dok;
+    a.nbad = d->nbad;
+    a.n = n;
+    a.xpow = d->xpow;
+    a.zero = d->zero;
+    (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
+    hipLaunchKernelGGL((mcrc_dev::k_spans<true, 1>), dim3(grid_for(*d, n)), dim3(kBlock),
+                       mcrc_dev::kLdsImage4Bytes, st, a, d->img);
+    unsigned long long bad = 0;
+    bool fail = hipGetLastError() != hipSuccess;
+    fail = fail || hipMemcpyAsync(&bad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st) != hipSuccess;
+    if (!dev) fail = fail || hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, st) != hipSuccess;
+    fail = fail || hipStreamSynchronize(st) != hipSuccess;
+    cleanup();
+    if (fail) return CRC32C_EHIP;
+    *nbad = bad;
+    return CRC32C_OK;
+}
+
+int crc32c_batch_multi(const crc32c_spans *s, int ngpus) {
+    if (!s) return CRC32C_EINVAL;
+    const int avail = crc32c_gpu_count();
+    if (avail <= 0) return CRC32C_ENODEV;
+    if (ngpus <= 0 || ngpus > avail) ngpus = avail;
+    // split by bytes: shard g gets spans whose cumulative length falls in its share
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < s->n; ++i) total += span_len(*s, i);
+    std::vector<uint64_t> cut(ngpus + 1, s->n);
+    cut[0] = 0;
+    uint64_t acc = 0, i = 0;
+    for (int g = 1; g < ngpus; ++g) {
+        const uint64_t target = total * g / ngpus;
+        while (i < s->n && acc < target) acc += span_len(*s, i++);
+        cut[g] = i;
+    }
+    std::vector<int> rcs(ngpus, CRC32C_OK);
+    std::vector<std::thread> th;
+    for (int g = 0; g < ngpus; ++g) {
+        th.emplace_back([&, g]() {
+            if (hipSetDevice(g) != hipSuccess) {
+                rcs[g] = CRC32C_EHIP;
+                return;
+            }
+            crc32c_spans sub = *s;
+            const uint64_t a0 = cut[g], a1 = cut[g + 1];
+            sub.n = a1 - a0;
+            if (sub.n == 0) return;
+            if (s->offsets) sub.offsets = s->offsets + a0;
+            else {
+                sub.base = (const uint8_t *)s->base + a0 * s->stride;
+                sub.base_bytes = s->base_bytes - a0 * s->stride;
+            }
+            if (s->lens) sub.lens = s->lens + a0;
+            if (s->crc_in) sub.crc_in = s->crc_in + a0;
+            sub.out = s->out + a0;
+            rcs[g] = crc32c_batch(&sub, 0, nullptr);
+        });
+    }
+    for (auto &t : th) t.join();
+    for (int rc : rcs)
+        if (rc) return rc;
+    return CRC32C_OK;
+}
+
+struct crc32c_job {
+    crc32c_spans spans;
+    unsigned flags;
+    int device;
+    std::thread worker;
+    int rc;
+};
+
+int crc32c_batch_submit(const crc32c_spans *s, unsigned flags, crc32c_job_t *job) {
+    if (!s || !job) return CRC32C_EINVAL;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return CRC32C_ENODEV;
+    crc32c_job *j = new crc32c_job();
+    j->spans = *s;
+    j->flags = flags & ~CRC32C_ASYNC;
+    j->device = dev;
+    j->rc = CRC32C_OK;
+    j->worker = std::thread([j]() {
+        if (hipSetDevice(j->device) != hipSuccess) {
+            j->rc = CRC32C_EHIP;
+            return;
+        }
+        j->rc = crc32c_batch(&j->spans, j->flags, nullptr);
+    });
+    *job = j;
+    return CRC32C_OK;
+}
+
+int crc32c_batch_wait(crc32c_job_t j) {
+    if (!j) return CRC32C_EINVAL;
+    j->worker.join();
+    const int rc = j->rc;
+    delete j;
+    return rc;
+}
+
+}  // extern "C"

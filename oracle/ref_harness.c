@@ -1,0 +1,57 @@
+/* ref_harness.c -- TEST/BASELINE INFRASTRUCTURE ONLY.
+ *
+ * Linked with the reference crc32c.c (compiled in place from /root/reference by
+ * oracle/Makefile into oracle/_ref/libref_crc32c.so).  Exposes the reference
+ * crc32c function pointer to ctypes and a pthread timing harness used for the
+ * cpu_baseline leg of bench.py: one thread per requested core, static
+ * contiguous split of the item array, each item checksummed with
+ * crc32c(0, item, len) exactly as storage.c:567 does.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <time.h>
+
+#include "crc32c.h"
+
+uint32_t ref_crc32c(uint32_t crc, const void *buf, size_t len) { return crc32c(crc, buf, len); }
+uint32_t ref_crc32c_sw(uint32_t crc, const void *buf, size_t len) { return crc32c_sw(crc, buf, len); }
+void ref_crc32c_init(void) { crc32c_init(); }
+
+struct job {
+    const unsigned char *base;
+    const uint64_t *offsets; /* NULL: base + i * stride */
+    const uint64_t *lens;    /* NULL: every item is `len` bytes */
+    uint64_t stride, len, lo, hi;
+    uint32_t *out;
+};
+
+static void *worker(void *arg) {
+    struct job *j = (struct job *)arg;
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        const unsigned char *p = j->base + (j->offsets ? j->offsets[i] : i * j->stride);
+        j->out[i] = crc32c(0, p, j->lens ? j->lens[i] : j->len);
+    }
+    return NULL;
+}
+
+/* Checksums n items with `threads` threads; returns wall seconds. */
+double ref_crc32c_batch_timed(const unsigned char *base, const uint64_t *offsets,
+                              const uint64_t *lens, uint64_t stride, uint64_t len, uint64_t n,
+                              int threads, uint32_t *out) {
+    if (threads < 1) threads = 1;
+    pthread_t *tid = calloc((size_t)threads, sizeof *tid);
+    struct job *jobs = calloc((size_t)threads, sizeof *jobs);
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (struct job){base, offsets, lens, stride, len, n * t / threads,
+                               n * (t + 1) / threads, out};
+        pthread_create(&tid[t], NULL, worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    free(tid);
+    free(jobs);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

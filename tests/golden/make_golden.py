@@ -1,0 +1,117 @@
+"""Generate the golden CRC-32C fixtures from the reference itself.
+
+Run in the build container (it needs oracle/_ref/libref_crc32c.so, which
+oracle/Makefile compiles from /root/reference/crc32c.c).  Every expected value
+below is the output of the reference ``crc32c`` function pointer after
+``crc32c_init()`` (hardware dispatch on an SSE4.2 host, crc32c.c:266-275) and
+is cross-checked against the reference ``crc32c_sw`` (crc32c.c:507-513).
+
+    python tests/golden/make_golden.py
+
+Outputs (committed):
+  kat.json     testapp.c:853-879 KATs, RFC 3720 B.4 vectors, "123456789"
+  spans.npz    4208 random bytes; crc32c(0, buf+off, len) and
+               crc32c(cin, buf+off, len) for len 0..4200, off 0..7
+  items.npz    memcached item images packed into wbufs (layout.py) with the
+               spill CRC (storage.c:567) of every item: config-1 shaped items
+               (key%07d, 4096-byte values, CAS) and items of varied geometry
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from memcached_amd import layout  # noqa: E402
+
+lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libref_crc32c.so"))
+lib.ref_crc32c_init()
+for fn in (lib.ref_crc32c, lib.ref_crc32c_sw):
+    fn.restype = ctypes.c_uint32
+    fn.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+
+
+def ref(crc: int, data) -> int:
+    b = bytes(data)
+    hw = lib.ref_crc32c(crc, b, len(b))
+    sw = lib.ref_crc32c_sw(crc, b, len(b))
+    assert hw == sw, (hw, sw)
+    return hw
+
+
+def main() -> None:
+    # --- known answers -----------------------------------------------------
+    buf256 = bytes(range(256))
+    kat = []
+    c1 = ref(0, buf256)
+    c2 = ref(c1, buf256)
+    c3 = ref(c2, buf256[1:255])
+    kat += [
+        {"name": "testapp_256", "crc_in": 0, "hex": buf256.hex(), "expect": c1, "ref_line": "testapp.c:861-864"},
+        {"name": "testapp_chain", "crc_in": c1, "hex": buf256.hex(), "expect": c2, "ref_line": "testapp.c:867-870"},
+        {"name": "testapp_odd", "crc_in": c2, "hex": buf256[1:255].hex(), "expect": c3, "ref_line": "testapp.c:873-876"},
+    ]
+    assert (c1, c2, c3) == (0x9C44184B, 0xAE10EE5A, 0xED37B906)
+    rfc = {"zeros32": bytes(32), "ones32": b"\xff" * 32, "inc32": bytes(range(32)),
+           "dec32": bytes(range(31, -1, -1)), "check": b"123456789", "empty": b""}
+    for name, data in rfc.items():
+        kat.append({"name": name, "crc_in": 0, "hex": data.hex(), "expect": ref(0, data)})
+    with open(os.path.join(HERE, "kat.json"), "w") as f:
+        json.dump(kat, f, indent=1)
+
+    # --- every length 0..4200 at every 8-byte alignment --------------------
+    rng = np.random.default_rng(20260715)
+    sbuf = rng.integers(0, 256, 4208, dtype=np.uint8)
+    crc0 = np.zeros((4201, 8), np.uint32)
+    crcin = np.zeros((4201, 8), np.uint32)
+    cin = rng.integers(0, 2**32, (4201, 8), dtype=np.uint64).astype(np.uint32)
+    raw = sbuf.tobytes()
+    for n in range(4201):
+        for off in range(8):
+            crc0[n, off] = ref(0, raw[off:off + n])
+            crcin[n, off] = ref(int(cin[n, off]), raw[off:off + n])
+    np.savez_compressed(os.path.join(HERE, "spans.npz"), buf=sbuf, crc0=crc0, cin=cin, crcin=crcin)
+
+    # --- memcached item images in wbufs -------------------------------------
+    def splitmix_bytes(seed: int, n: int) -> bytes:
+        out = bytearray()
+        z = seed
+        while len(out) < n:
+            z = (z + 0x9E3779B97F4A7C15) & (2**64 - 1)
+            x = z
+            x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+            x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+            out += (x ^ (x >> 31)).to_bytes(8, "little")
+        return bytes(out[:n])
+
+    cfg1 = [layout.make_item(b"key%07d" % i, splitmix_bytes(1 + i, 4096), cas=i + 1) for i in range(16)]
+    vrng = np.random.default_rng(7)
+    varied = []
+    for i in range(120):
+        klen = int(vrng.integers(1, 250))
+        vlen = int(vrng.integers(0, 6000))
+        cas = int(vrng.integers(1, 2**63)) if vrng.random() < 0.7 else None
+        cfl = int(vrng.integers(1, 2**32)) if vrng.random() < 0.3 else 0
+        key = bytes(vrng.integers(33, 127, klen, dtype=np.uint8))
+        varied.append(layout.make_item(key, bytes(vrng.integers(0, 256, vlen, dtype=np.uint8)),
+                                       cas=cas, client_flags=cfl, time_hash=int(vrng.integers(0, 2**32))))
+    out = {}
+    for name, items, wsz in (("cfg1", cfg1, 64 * 1024), ("varied", varied, 128 * 1024)):
+        buf, offs = layout.pack_wbufs(items, wsz)
+        soffs, slens = layout.spans_of(buf, offs)
+        crcs = np.array([ref(0, buf[int(o):int(o) + int(n)]) for o, n in zip(soffs, slens)], np.uint32)
+        layout.store_crcs(buf, offs, crcs)
+        out[f"{name}_buf"], out[f"{name}_offsets"], out[f"{name}_crc"] = buf, offs, crcs
+        out[f"{name}_wbuf"] = np.uint64(wsz)
+    np.savez_compressed(os.path.join(HERE, "items.npz"), **out)
+    print("wrote kat.json spans.npz items.npz")
+
+
+if __name__ == "__main__":
+    main()

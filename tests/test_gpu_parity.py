@@ -1,0 +1,194 @@
+"""GPU parity: every kernel, through the C-ABI (libmcrc32c.so), against the
+CPU oracle and the reference-generated golden vectors.  Bit-exact."""
+import os
+
+import numpy as np
+import pytest
+
+try:  # GPU processes load torch (and its HIP runtime) before libmcrc32c.so
+    import torch as _torch  # noqa: F401
+except ImportError:
+    pass
+
+from memcached_amd import _lib, layout
+from memcached_amd import crc32c as mc
+
+from . import oracle
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need a visible MI355X"
+    assert mc.gpu_count() >= 1, "libmcrc32c.so sees no gfx950 device"
+    return t
+
+
+def _dev(torch, arr):
+    return torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+
+
+def _u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def test_fixed_4096_k1(torch):
+    rng = np.random.default_rng(42)
+    n = 4099  # not a multiple of the 32 spans per block step
+    host = rng.integers(0, 256, n * 4096, dtype=np.uint8)
+    want = oracle.batch(host, np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096))
+    d = _dev(torch, host)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = _lib.Spans(d.data_ptr(), host.size, None, 4096, None, 4096, None, out.data_ptr(), n)
+    import ctypes
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None))
+    assert _lib.lib.crc32c_last_kernel_ms() > 0
+    np.testing.assert_array_equal(_u32(out), want)
+    # with per-item initial CRCs
+    cin = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dcin = _dev(torch, cin.view(np.int32))
+    s.crc_in = dcin.data_ptr()
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None))
+    want_in = oracle.batch(host, np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096), cin)
+    np.testing.assert_array_equal(_u32(out), want_in)
+
+
+def test_golden_all_lengths_alignments(torch):
+    g = np.load(os.path.join(GOLD, "spans.npz"))
+    buf = g["buf"]
+    L, A = g["crc0"].shape
+    offs = np.tile(np.arange(A, dtype=np.uint64), L)
+    lens = np.repeat(np.arange(L, dtype=np.uint32), A)
+    d = _dev(torch, buf)
+    out = mc.batch(d, offsets=_dev(torch, offs.view(np.int64)), lens=_dev(torch, lens.view(np.int32)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), g["crc0"].reshape(-1))
+    cin = g["cin"].reshape(-1)
+    out = mc.batch(d, offsets=_dev(torch, offs.view(np.int64)), lens=_dev(torch, lens.view(np.int32)),
+                   crc_in=_dev(torch, cin.view(np.int32)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), g["crcin"].reshape(-1))
+
+
+def test_golden_host_path():
+    g = np.load(os.path.join(GOLD, "spans.npz"))
+    L, A = g["crc0"].shape
+    offs = np.tile(np.arange(A, dtype=np.uint64), L)
+    lens = np.repeat(np.arange(L, dtype=np.uint32), A)
+    order = np.argsort(offs, kind="stable")  # host batches need non-decreasing offsets
+    out = mc.batch(g["buf"], offsets=offs[order], lens=lens[order], crc_in=g["cin"].reshape(-1)[order])
+    np.testing.assert_array_equal(out, g["crcin"].reshape(-1)[order])
+
+
+def test_aligned_spans_kernel(torch):
+    rng = np.random.default_rng(5)
+    n = 3000
+    lens = (rng.integers(0, 700, n) * 16).astype(np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 16 * rng.integers(0, 3, n - 1))]).astype(np.uint64)
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1] + 64), dtype=np.uint8)
+    want = oracle.batch(host, offs, lens)
+    d = _dev(torch, host)
+    out = mc.batch(d, offsets=_dev(torch, offs.view(np.int64)), lens=_dev(torch, lens.view(np.int32)),
+                   aligned16=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), want)
+
+
+def test_variable_unaligned_up_to_1mib(torch):
+    rng = np.random.default_rng(7)
+    classes = np.array([int(64 * 1.25 ** k) for k in range(44) if 64 * 1.25 ** k <= 1 << 20])
+    p = 1.0 / np.arange(1, classes.size + 1)
+    n = 2500
+    cls = rng.choice(classes.size, n, p=p / p.sum())
+    lens = (classes[cls] * rng.uniform(0.9, 1.1, n)).astype(np.uint32) + rng.integers(0, 16, n).astype(np.uint32)
+    lens[:5] = [0, 1, 2, 3, (1 << 20) + 37]
+    offs = np.concatenate([[3], 3 + np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1] + 5), dtype=np.uint8)
+    cin = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(host, offs, lens, cin)
+    d = _dev(torch, host)
+    out = mc.batch(d, offsets=_dev(torch, offs.view(np.int64)), lens=_dev(torch, lens.view(np.int32)),
+                   crc_in=_dev(torch, cin.view(np.int32)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), want)
+    # the same batch through the host staging path and the multi-GPU splitter
+    np.testing.assert_array_equal(mc.batch(host, offsets=offs, lens=lens, crc_in=cin), want)
+    np.testing.assert_array_equal(mc.batch_multi(host, offsets=offs, lens=lens, crc_in=cin), want)
+
+
+def test_realistic_item_spans_4133(torch):
+    """config-1/config-5 geometry: 4133-byte spans at +32 of 4165-byte images."""
+    items = [layout.make_item(b"key%07d" % i, np.random.default_rng(i).integers(0, 256, 4096, dtype=np.uint8).tobytes(),
+                              cas=i + 1) for i in range(700)]
+    buf, offs = layout.pack_wbufs(items, 1 << 20)
+    soffs, slens = layout.spans_of(buf, offs)
+    assert (slens == 4133).all()
+    want = oracle.batch(buf, soffs, slens)
+    d = _dev(torch, buf)
+    out = mc.batch(d, offsets=_dev(torch, soffs.view(np.int64)), lens=_dev(torch, slens.astype(np.uint32).view(np.int32)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), want)
+
+
+@pytest.mark.parametrize("name", ["cfg1", "varied"])
+def test_verify_golden_items(torch, name):
+    g = np.load(os.path.join(GOLD, "items.npz"))
+    buf, offs = g[f"{name}_buf"].copy(), g[f"{name}_offsets"]
+    ok, nbad = mc.verify_items(_dev(torch, buf), _dev(torch, offs.view(np.int64)))
+    assert nbad == 0 and ok.cpu().numpy().all()
+    ok, nbad = mc.verify_items(buf, offs)  # host path
+    assert nbad == 0 and ok.all()
+    # flip one bit in 3 items: exactly those fail (the reference has no such test)
+    rng = np.random.default_rng(11)
+    victims = rng.choice(offs.size, 3, replace=False)
+    for v in victims:
+        o = int(offs[v])
+        buf[o + 32 + int(rng.integers(0, layout.ntotal_of(buf, o) - 32))] ^= 1 << int(rng.integers(0, 8))
+    ok, nbad = mc.verify_items(buf, offs)
+    assert nbad == 3
+    assert sorted(np.flatnonzero(ok == 0).tolist()) == sorted(victims.tolist())
+
+
+def test_empty_batch_and_zero_lengths(torch):
+    d = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    out = mc.batch(d, offsets=torch.zeros(0, dtype=torch.int64, device="cuda"),
+                   lens=torch.zeros(0, dtype=torch.int32, device="cuda"))
+    assert out.numel() == 0
+    cin = np.array([0, 1, 0xFFFFFFFF, 0x12345678], np.uint32)
+    out = mc.batch(d, offsets=torch.tensor([0, 5, 17, 63], device="cuda"),
+                   lens=torch.zeros(4, dtype=torch.int32, device="cuda"),
+                   crc_in=_dev(torch, cin.view(np.int32)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), cin)  # crc32c(c, "", 0) == c
+
+
+def test_full_size_config2(torch):
+    """BASELINE config 2 at full size: 1 M x 4 KiB, every CRC checked."""
+    n, L = 1 << 20, 4096
+    g = torch.Generator(device="cuda").manual_seed(42)
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    import ctypes
+    s = _lib.Spans(d.data_ptr(), n * L, None, L, None, L, None, out.data_ptr(), n)
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None))
+    host = d.cpu().numpy()
+    want = oracle.batch(host, np.arange(n, dtype=np.uint64) * L, np.full(n, L))
+    np.testing.assert_array_equal(_u32(out), want)
+
+
+def test_async_submit_wait():
+    import ctypes
+    rng = np.random.default_rng(9)
+    host = rng.integers(0, 256, 1 << 22, dtype=np.uint8)
+    offs = np.arange(0, host.size - 5000, 5000, dtype=np.uint64) + 1
+    lens = np.full(offs.size, 4999, np.uint32)
+    out = np.empty(offs.size, np.uint32)
+    s = _lib.Spans(host.ctypes.data, host.size, offs.ctypes.data, 0, lens.ctypes.data, 0, None, out.ctypes.data,
+                   offs.size)
+    job = ctypes.c_void_p()
+    _lib.check(_lib.lib.crc32c_batch_submit(ctypes.byref(s), 0, ctypes.byref(job)))
+    _lib.check(_lib.lib.crc32c_batch_wait(job))
+    np.testing.assert_array_equal(out, oracle.batch(host, offs, lens))

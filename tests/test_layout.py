@@ -1,0 +1,32 @@
+"""Item layout mirror (memcached_amd/layout.py) against the oracle's walk."""
+import numpy as np
+
+from memcached_amd import layout
+
+from . import oracle
+
+
+def test_ntotal_of_config1_item():
+    img = layout.make_item(b"key0000001", b"x" * 4096, cas=5)
+    assert len(img) == 4165  # 48 + 10 + 1 + 4098 + 8
+    assert layout.ntotal_of(img, 0) == 4165
+
+
+def test_pack_walk_roundtrip():
+    rng = np.random.default_rng(3)
+    items = [layout.make_item(b"k%05d" % i, rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes(),
+                              cas=None if i % 3 else i, client_flags=i % 5) for i in range(300)]
+    buf, offs = layout.pack_wbufs(items, 64 * 1024)
+    soffs, slens = layout.spans_of(buf, offs)
+    crcs = oracle.batch(buf, soffs, slens)
+    layout.store_crcs(buf, offs, crcs)
+    found = []
+    for w in range(0, buf.size, 64 * 1024):
+        o, ok = oracle.verify_span(buf[w:w + 64 * 1024])
+        assert ok.all()
+        found += [w + int(x) for x in o]
+    assert found == [int(x) for x in offs]
+    # one flipped bit is detected
+    buf[int(offs[7]) + 100] ^= 0x10
+    o, ok = oracle.verify_span(buf[:64 * 1024])
+    assert (~ok.astype(bool)).sum() == 1

@@ -1,0 +1,175 @@
+// ubench.hip -- standalone microbenchmark for the fixed-length CRC kernel
+// variants (no torch).  Dev tool: measures read bandwidth of each load pattern
+// (LOAD_ONLY) and full CRC throughput, and checks every item against the
+// shim's host CRC.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../memcached_amd/csrc/crc32c_gf2.h"
+#include "../memcached_amd/csrc/crc32c_host.h"
+#include "../memcached_amd/csrc/crc32c_kernels.hip"
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, \
+                    __LINE__);                                                         \
+            exit(1);                                                                   \
+        }                                                                              \
+    } while (0)
+
+__global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = seed + (i + 1) * 0x9e3779b97f4a7c15ull;
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_read(const uint4 *__restrict__ p, uint64_t n16,
+                                                uint32_t *__restrict__ sink) {
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^
+               d.z ^ d.w;
+    }
+    for (; i < n16; i += stride) acc ^= p[i].x ^ p[i].y ^ p[i].z ^ p[i].w;
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+struct Variant {
+    const char *name;
+    int slice, lpi, ch;
+    bool load_only;
+    void (*kern)(const uint8_t *, uint64_t, uint64_t, const uint4 *, uint32_t, uint32_t,
+                 const uint32_t *, uint32_t *);
+};
+#define V(S, L, C, R, M) \
+    {#S "_l" #L "_c" #C "_r" #R "_m" #M, S, L, C, M == 1, mcrc_dev::k_fixed<S, L, C, R, M>}
+#define V3(S, L, C, R, M) \
+    {#S "_l" #L "_c" #C "_r" #R "_m" #M "_d3", S, L, C, M == 1, mcrc_dev::k_fixed<S, L, C, R, M, 3>}
+
+int main(int argc, char **argv) {
+    const uint64_t nitems = argc > 1 ? strtoull(argv[1], 0, 0) : (1ull << 20);
+    const uint32_t len = 4096;
+    const int iters = argc > 2 ? atoi(argv[2]) : 10;
+    const char *only = argc > 3 ? argv[3] : nullptr;  // substring filter on variant names
+    const int only_bs = argc > 4 ? atoi(argv[4]) : 0;
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    printf("device %s CUs %d\n", prop.name, prop.multiProcessorCount);
+    const uint64_t bytes = nitems * len;
+    uint8_t *d_buf;
+    uint32_t *d_out, *d_sink;
+    CK(hipMalloc(&d_buf, bytes));
+    CK(hipMalloc(&d_out, nitems * 4));
+    CK(hipMalloc(&d_sink, 64));
+    k_fill<<<4096, 256>>>((uint64_t *)d_buf, bytes / 8, 42);
+    CK(hipDeviceSynchronize());
+
+    std::vector<uint8_t> h_buf(bytes);
+    CK(hipMemcpy(h_buf.data(), d_buf, bytes, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> want(nitems);
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t i = 0; i < nitems; ++i) want[i] = mcrc::crc32c_host_hw(0, &h_buf[i * len], len);
+    auto t1 = std::chrono::steady_clock::now();
+    printf("host crc (1 core): %.2f GiB/s\n",
+           bytes / std::chrono::duration<double>(t1 - t0).count() / (1 << 30));
+
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    if (!only) {
+        const int grid = prop.multiProcessorCount * 2;
+        for (int w = 0; w < 2; ++w) k_read<<<grid, 1024>>>((const uint4 *)d_buf, bytes / 16, d_sink);
+        CK(hipEventRecord(e0));
+        for (int it = 0; it < iters; ++it)
+            k_read<<<grid, 1024>>>((const uint4 *)d_buf, bytes / 16, d_sink);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= iters;
+        printf("%-28s %8.3f ms  %8.1f GB/s\n", "read_dwordx4_coalesced", ms, bytes / ms / 1e6);
+    }
+
+    Variant vars[] = {
+        V(4, 32, 32, 4, 0), V(4, 32, 64, 2, 0), V(1, 64, 32, 2, 0),
+        V3(4, 32, 32, 4, 0), V3(4, 32, 64, 2, 0), V3(4, 64, 32, 2, 0), V3(1, 64, 32, 2, 0),
+        V3(4, 64, 16, 4, 0), V3(1, 64, 16, 4, 0), V3(4, 32, 32, 4, 3),
+    };
+    std::vector<uint32_t> img(mcrc::kImage4Dwords);
+    uint4 *d_img;
+    CK(hipMalloc(&d_img, mcrc::kImage4Dwords * 4));
+    const uint32_t kfinal = ~mcrc::Gf2Op::zeros(len).apply(0xffffffffu);
+    const uint32_t kspan = mcrc::xpow8n(len);
+    std::vector<uint32_t> got(nitems);
+    for (const Variant &v : vars) {
+        if (only && !strstr(v.name, only)) continue;
+        uint32_t lds_bytes;
+        if (v.slice == 1) {
+            mcrc::build_lds_image1(img.data(), v.ch, v.lpi);
+            lds_bytes = mcrc_dev::kLdsImage1Bytes;
+        } else {
+            mcrc::build_lds_image4(img.data(), v.ch, v.lpi);
+            lds_bytes = mcrc_dev::kLdsImage4Bytes;
+        }
+        CK(hipMemcpy(d_img, img.data(), lds_bytes, hipMemcpyHostToDevice));
+        CK(hipFuncSetAttribute((const void *)v.kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               lds_bytes));
+        for (int pass = 0; pass < 3; ++pass) {
+            const bool with_crc_in = pass == 1;
+            const bool hot = pass == 2;  // stride 0: every item is item 0 (cache-resident)
+            if (with_crc_in && (v.load_only || only_bs)) continue;
+            const uint64_t istride = hot ? 0 : len;
+            const int bs = 1024;
+            const int grid = prop.multiProcessorCount * (v.slice == 1 ? 2 : 1);
+            std::vector<uint32_t> cin(nitems);
+            uint32_t *d_cin = nullptr;
+            if (with_crc_in) {
+                for (uint64_t i = 0; i < nitems; ++i) cin[i] = (uint32_t)(i * 2654435761u);
+                CK(hipMalloc(&d_cin, nitems * 4));
+                CK(hipMemcpy(d_cin, cin.data(), nitems * 4, hipMemcpyHostToDevice));
+            }
+            CK(hipMemset(d_out, 0, nitems * 4));
+            v.kern<<<grid, bs, lds_bytes>>>(d_buf, istride, nitems, d_img, kfinal, kspan, d_cin, d_out);
+            CK(hipGetLastError());
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0));
+            for (int it = 0; it < iters; ++it)
+                v.kern<<<grid, bs, lds_bytes>>>(d_buf, istride, nitems, d_img, kfinal, kspan, d_cin,
+                                                d_out);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= iters;
+            uint64_t bad = 0;
+            if (!v.load_only) {
+                CK(hipMemcpy(got.data(), d_out, nitems * 4, hipMemcpyDeviceToHost));
+                for (uint64_t i = 0; i < nitems; ++i) {
+                    const uint32_t w = hot           ? want[0]
+                                       : with_crc_in ? mcrc::crc32c_host_hw(cin[i], &h_buf[i * len], len)
+                                                     : want[i];
+                    bad += got[i] != w;
+                }
+            }
+            printf("%-22s %s %8.3f ms  %8.1f GB/s  %5.1f%% of 8TB/s  bad=%llu\n", v.name,
+                   with_crc_in ? "crc_in" : hot ? "hot   " : "      ", ms, bytes / ms / 1e6,
+                   bytes / ms / 1e6 / 8000 * 100, (unsigned long long)bad);
+            if (d_cin) CK(hipFree(d_cin));
+        }
+    }
+    return 0;
+}
