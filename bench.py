@@ -46,16 +46,23 @@ def shard(n_total: int, rank: int, world: int):
     return lo, hi
 
 
-def dist_setup(n_gpus: int):
+def dist_setup(n_gpus: int, backend: str = "nccl"):
+    """One process per GPU; RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the
+    launcher.  The process group only carries the timing barrier and the
+    max-over-ranks reduction ("nccl" is RCCL on ROCm; "gloo" for CPU tests)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n_gpus:
         raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    if backend == "nccl":
+        torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return rank, world, local
 
 
@@ -69,9 +76,21 @@ def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def timed(step, steps: int, world: int, sync=torch.cuda.synchronize):
+    """Barrier + sync, run `steps` steps, sync + barrier; max wall time over ranks."""
+    barrier(world)
+    sync()
+    t0 = time.perf_counter()
+    r = step(steps)
+    sync()
+    barrier(world)
+    return max_over_ranks(time.perf_counter() - t0, world), r
 
 
 def make_batch(n: int, seed: int):
@@ -165,14 +184,7 @@ def main():
         pass
     torch.cuda.synchronize()
 
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    evs = run_steps(spans, args.steps, stream)
-    torch.cuda.synchronize()
-    barrier(world)
-    t1 = time.perf_counter()
-    elapsed = max_over_ranks(t1 - t0, world)
+    elapsed, evs = timed(lambda k: run_steps(spans, k, stream), args.steps, world)
 
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     kernel_ms = max_over_ranks(kernel_ms, world)
@@ -196,7 +208,7 @@ def main():
         "data": "synthetic (torch.randint bytes, seed 42 + rank), device-resident",
         "config": {
             "workload": "BASELINE configs[1]: 1 Mi items x 4096 B per GPU, stride 4096, one 32-lane group per "
-                        "item (K1 k_fixed<slice-by-4, 32 lanes, 64 B/lane/row, 2 rows>)",
+                        "item (K1 k_fixed<slice-by-4, 32 lanes, 32 B/lane/row, 4 rows, bitop3 + DPP merge>)",
             "items_per_gpu": n,
             "item_bytes": ITEM_BYTES,
             "parallelism": f"items sharded across {world} rank(s), no collective on the data path",

@@ -98,6 +98,21 @@ struct Step<4> {
     }
 };
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Slice-by-4 step fused with the next data dword: returns
+//   T3[x0] ^ T2[x1] ^ T1[x2] ^ T0[x3] ^ w_next
+// with two v_bitop3 (3-input XOR) instead of four v_xor.
+__device__ __forceinline__ uint32_t step4_next(uint32_t x, uint32_t w_next, const LaneCtx &c) {
+    const uint32_t a3 = lds_ld(__builtin_amdgcn_perm(x, c.lane4, 0x0c0c0400u) + kAux4Bytes);
+    const uint32_t a2 = lds_ld(__builtin_amdgcn_perm(x, c.lane4, 0x0c0c0500u) + kAux4Bytes + 128u);
+    const uint32_t a1 = lds_ld(__builtin_amdgcn_perm(x, c.lane4hi, 0x0c020600u) + kAux4Bytes);
+    const uint32_t a0 = lds_ld(__builtin_amdgcn_perm(x, c.lane4hi, 0x0c020700u) + kAux4Bytes + 128u);
+    return xor3(xor3(a3, a2, a1), a0, w_next);
+}
+
 // Apply the zeros operator stored in aux tables t0..t0+3.
 template <int SLICE>
 __device__ __forceinline__ uint32_t apply_op(uint32_t t0, uint32_t v) {
@@ -116,6 +131,33 @@ __device__ __forceinline__ uint32_t group_reduce(uint32_t v, uint32_t lane) {
         if ((lane & ((2u << k) - 1u)) == 0) v = apply_op<SLICE>(kAuxTree + 4 * k, v) ^ x;
     }
     return v;
+}
+
+// Value of lane (l + 2^k) for lanes whose partner stays inside a 32-lane
+// group: DPP row shifts for k <= 3, v_permlane16_swap for k = 4.  No LDS.
+template <int K>
+__device__ __forceinline__ uint32_t lane_down(uint32_t v) {
+    if constexpr (K < 4) {
+        return __builtin_amdgcn_update_dpp(0u, v, 0x100 | (1 << K), 0xf, 0xf, false);  // row_shl:2^K
+    } else {
+        static_assert(K == 4, "groups are 32 lanes");
+        return __builtin_amdgcn_permlane16_swap(v, v, false, false)[1];  // row r gets row r^1
+    }
+}
+
+// group_reduce for LPI = 32 with DPP / permlane lane moves (slice-by-4 aux).
+template <int K = 0>
+__device__ __forceinline__ uint32_t group_reduce32_dpp(uint32_t v, uint32_t lane) {
+    if constexpr (K == 5) {
+        return v;
+    } else {
+        const uint32_t x = lane_down<K>(v);
+        if ((lane & ((2u << K) - 1u)) == 0) v = xor3(Step<4>::aux(kAuxTree + 4 * K, v & 0xffu) ^ x,
+                                                      Step<4>::aux(kAuxTree + 4 * K + 1, (v >> 8) & 0xffu),
+                                                      Step<4>::aux(kAuxTree + 4 * K + 2, (v >> 16) & 0xffu)) ^
+                                                 Step<4>::aux(kAuxTree + 4 * K + 3, v >> 24);
+        return group_reduce32_dpp<K + 1>(v, lane);
+    }
 }
 
 // Copy a table image from global memory into this workgroup's LDS.

@@ -20,6 +20,10 @@ namespace mcrc_dev {
 // K1: fixed-length aligned items
 // ===========================================================================
 
+__device__ __forceinline__ uint32_t dw4(const uint4 &v, int k) {
+    return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+}
+
 // One lane's share of one item: R rows x CH bytes, 16-B loads.
 template <int LPI, int CH, int R>
 struct ItemRegs {
@@ -71,6 +75,68 @@ __device__ __forceinline__ uint32_t lane_partial(const ItemRegs<LPI, CH, R> &it,
     return a;
 }
 
+// Lane partial for SLICE 4, LPI 32: chains fused with bitop3 XORs.
+template <int CH, int R>
+__device__ __forceinline__ uint32_t lane_partial_x3(const ItemRegs<32, CH, R> &it, const LaneCtx &c) {
+    constexpr int Q = CH / 16;
+    constexpr int N = 4 * Q;  // dwords per chain
+    uint32_t x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = it.d[r][0].x;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t wn = i + 1 < N ? dw4(it.d[r][(i + 1) >> 2], (i + 1) & 3) : 0u;
+            x[r] = step4_next(x[r], wn, c);
+        }
+    }
+    uint32_t a = x[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) a = apply_op<4>(kAuxOp5, a) ^ x[r];
+    return a;
+}
+
+// Same as lane_partial_x3, but the loads of the NEXT step (into `nxt`) are
+// issued one at a time between dword steps of this chain, so the vector
+// memory queue is fed steadily instead of in one burst per step.
+template <int CH, int R>
+__device__ __forceinline__ uint32_t lane_partial_x3_feed(const ItemRegs<32, CH, R> &it, const LaneCtx &c,
+                                                         ItemRegs<32, CH, R> &nxt, const uint8_t *np,
+                                                         uint32_t li) {
+    constexpr int Q = CH / 16;
+    constexpr int N = 4 * Q;       // dwords per chain
+    constexpr int NL = R * Q;      // loads per step
+    constexpr int EVERY = N / NL > 0 ? N / NL : 1;
+    uint32_t x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = it.d[r][0].x;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        if (i % EVERY == 0 && i / EVERY < NL) {
+            constexpr int dummy = 0;
+            (void)dummy;
+            const int l = i / EVERY, r = l / Q, q = l % Q;
+            nxt.d[r][q] = *reinterpret_cast<const uint4 *>(np + (size_t)r * 32 * CH + li * CH + 16 * q);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t wn = i + 1 < N ? dw4(it.d[r][(i + 1) >> 2], (i + 1) & 3) : 0u;
+            x[r] = step4_next(x[r], wn, c);
+        }
+    }
+#pragma unroll
+    for (int l = (N + EVERY - 1) / EVERY; l < NL; ++l) {
+        const int r = l / Q, q = l % Q;
+        nxt.d[r][q] = *reinterpret_cast<const uint4 *>(np + (size_t)r * 32 * CH + li * CH + 16 * q);
+    }
+    uint32_t a = x[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) a = apply_op<4>(kAuxOp5, a) ^ x[r];
+    return a;
+}
+
 // Persistent grid-stride loop; each wave handles 64/LPI items per step and
 // loads the next step's items before reducing the current ones (register
 // ping-pong, no copies).
@@ -78,7 +144,9 @@ __device__ __forceinline__ uint32_t lane_partial(const ItemRegs<LPI, CH, R> &it,
 //   kfinal = ~M_len(0xffffffff), kspan = x^(8*len) mod P.
 // MODE 0: full CRC.  Ablations for profiling (wrong results by design):
 // MODE 1: loads only; MODE 2: no lane-group reduction; MODE 3: data chains only.
-template <int SLICE, int LPI, int CH, int R, int MODE, int DEPTH = 2>
+// MODE 4/5: full CRC, optimised variants (SLICE 4, LPI 32 only).
+// MODE 6: MODE 5 with the next step's loads spread over the chains.
+template <int SLICE, int LPI, int CH, int R, int MODE, int DEPTH = 2, int STAGGER = 0>
 __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base, uint64_t stride,
                                                 uint64_t nitems, const uint4 *__restrict__ img,
                                                 uint32_t kfinal, uint32_t kspan,
@@ -98,6 +166,11 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     const uint64_t ngroups = (nitems + IPW - 1) / IPW;
     uint64_t grp = blockIdx.x * waves + (threadIdx.x >> 6);
     if (grp >= ngroups) return;
+    if constexpr (STAGGER > 0) {
+        // desynchronise the workgroup's waves: odd waves start STAGGER x 8K cycles late
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 1u)
+            for (int i = 0; i < STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+    }
 
     auto item_of = [&](uint64_t gi) { return gi * IPW + g; };
     auto clamp = [&](uint64_t it) { return it < nitems ? it : nitems - 1; };
@@ -109,7 +182,11 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
             return;
         }
         uint32_t raw;
-        if (MODE == 3)
+        if (MODE == 5)  // optimised: bitop3 chains + DPP reduction (SLICE 4, LPI 32)
+            raw = group_reduce32_dpp(lane_partial_x3<CH, R>(regs, c), lane);
+        else if (MODE == 4)  // bitop3 chains, LDS-shuffle reduction
+            raw = group_reduce<SLICE, LPI>(lane_partial_x3<CH, R>(regs, c), lane);
+        else if (MODE == 3)
             raw = lane_partial<SLICE, LPI, CH, R, false>(regs, c);
         else if (MODE == 2)
             raw = lane_partial<SLICE, LPI, CH, R>(regs, c);
@@ -122,7 +199,25 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 
     auto addr = [&](uint64_t gi) { return base + clamp(item_of(gi < ngroups ? gi : ngroups - 1)) * stride; };
     ItemRegs<LPI, CH, R> ra, rb;
-    if (DEPTH == 2) {
+    if constexpr (MODE == 6) {
+        // loads of the next step interleaved with this step's chains
+        auto fin6 = [&](const ItemRegs<LPI, CH, R> &cur, ItemRegs<LPI, CH, R> &nxt, uint64_t gi) {
+            const uint64_t item = item_of(gi);
+            const uint32_t raw =
+                group_reduce32_dpp(lane_partial_x3_feed<CH, R>(cur, c, nxt, addr(gi + gstep), li), lane);
+            if (li == 0 && item < nitems)
+                out[item] = crc_in ? ~(mulmodp_dev(~crc_in[item], kspan) ^ raw) : raw ^ kfinal;
+        };
+        ra.load(addr(grp), li);
+        for (;;) {
+            fin6(ra, rb, grp);
+            grp += gstep;
+            if (grp >= ngroups) break;
+            fin6(rb, ra, grp);
+            grp += gstep;
+            if (grp >= ngroups) break;
+        }
+    } else if (DEPTH == 2) {
         ra.load(addr(grp), li);
         for (;;) {
             rb.load(addr(grp + gstep), li);

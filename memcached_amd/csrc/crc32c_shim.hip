@@ -50,7 +50,9 @@ namespace {
 
 constexpr int kBlock = 1024;                    // 16 waves, 32 lane groups
 constexpr uint32_t kItemsPerBlockStep = 32;     // one span per 32-lane group
-constexpr uint32_t kFixedLen = 4096;            // K1 instance: 2 rows x 32 lanes x 64 B
+constexpr uint32_t kFixedLen = 4096;            // K1 instance: 4 rows x 32 lanes x 32 B
+constexpr uint32_t kFixedCH = 32;
+#define K1_KERNEL mcrc_dev::k_fixed<4, 32, kFixedCH, 4, 5>
 
 thread_local float g_last_kernel_ms = -1.0f;
 
@@ -58,7 +60,8 @@ struct Device {
     int id = -1;
     int cus = 0;
     bool ok = false;
-    uint4 *img = nullptr;       // LDS table image (CH = 64)
+    uint4 *img = nullptr;       // LDS table image for the span kernels (CH = 64)
+    uint4 *img_k1 = nullptr;    // LDS table image for K1 (CH = 32)
     uint32_t *xpow = nullptr;   // 3 x 1024 x^(8n) table
     uint4 *zero = nullptr;      // 16 zero bytes
     unsigned long long *nbad = nullptr;
@@ -113,6 +116,9 @@ int init_device(Device &d, int id) {
     }
     HIP_OK(hipMalloc(&d.img, img.size() * 4));
     HIP_OK(hipMemcpy(d.img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
+    mcrc::build_lds_image4(img.data(), kFixedCH);
+    HIP_OK(hipMalloc(&d.img_k1, img.size() * 4));
+    HIP_OK(hipMemcpy(d.img_k1, img.data(), img.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&d.xpow, xp.size() * 4));
     HIP_OK(hipMemcpy(d.xpow, xp.data(), xp.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&d.zero, 64));
@@ -123,7 +129,7 @@ int init_device(Device &d, int id) {
     HIP_OK(hipEventCreate(&d.ev0));
     HIP_OK(hipEventCreate(&d.ev1));
     const void *kernels[] = {
-        (const void *)mcrc_dev::k_fixed<4, 32, 64, 2, 0>,  (const void *)mcrc_dev::k_spans<false, 0>,
+        (const void *)K1_KERNEL,                            (const void *)mcrc_dev::k_spans<false, 0>,
         (const void *)mcrc_dev::k_spans<true, 0>,           (const void *)mcrc_dev::k_spans<true, 1>,
     };
     for (const void *k : kernels)
@@ -165,9 +171,8 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
     const uint32_t kspan = fixed ? mcrc::xpow8n(s.len) : 0u;
     if (fixed && s.len == kFixedLen && aligned16(s.base) && (s.stride & 15u) == 0) {
         const uint32_t kfinal = ~mcrc::Gf2Op::zeros(s.len).apply(0xffffffffu);
-        hipLaunchKernelGGL((mcrc_dev::k_fixed<4, 32, 64, 2, 0>), dim3(grid_for(d, s.n)), dim3(kBlock),
-                           mcrc_dev::kLdsImage4Bytes, st, (const uint8_t *)s.base, s.stride, s.n,
-                           d.img, kfinal, kspan, s.crc_in, s.out);
+        hipLaunchKernelGGL((K1_KERNEL), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImage4Bytes, st,
+                           (const uint8_t *)s.base, s.stride, s.n, d.img_k1, kfinal, kspan, s.crc_in, s.out);
     } else {
         mcrc_dev::SpanArgs a{};
         a.base = (const uint8_t *)s.base;

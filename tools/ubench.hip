@@ -57,6 +57,8 @@ struct Variant {
 };
 #define V(S, L, C, R, M) \
     {#S "_l" #L "_c" #C "_r" #R "_m" #M, S, L, C, M == 1, mcrc_dev::k_fixed<S, L, C, R, M>}
+#define VS(S, L, C, R, M, ST) \
+    {#S "_l" #L "_c" #C "_r" #R "_m" #M "_st" #ST, S, L, C, M == 1, mcrc_dev::k_fixed<S, L, C, R, M, 2, ST>}
 #define V3(S, L, C, R, M) \
     {#S "_l" #L "_c" #C "_r" #R "_m" #M "_d3", S, L, C, M == 1, mcrc_dev::k_fixed<S, L, C, R, M, 3>}
 
@@ -105,9 +107,8 @@ int main(int argc, char **argv) {
     }
 
     Variant vars[] = {
-        V(4, 32, 32, 4, 0), V(4, 32, 64, 2, 0), V(1, 64, 32, 2, 0),
-        V3(4, 32, 32, 4, 0), V3(4, 32, 64, 2, 0), V3(4, 64, 32, 2, 0), V3(1, 64, 32, 2, 0),
-        V3(4, 64, 16, 4, 0), V3(1, 64, 16, 4, 0), V3(4, 32, 32, 4, 3),
+        V(4, 32, 64, 2, 5), V(4, 32, 32, 4, 5), V(4, 32, 16, 8, 5), V(4, 32, 16, 8, 0),
+        V(4, 32, 16, 8, 3), V(4, 32, 32, 4, 3), V(4, 32, 16, 8, 1), V(4, 32, 64, 2, 1),
     };
     std::vector<uint32_t> img(mcrc::kImage4Dwords);
     uint4 *d_img;
@@ -119,10 +120,10 @@ int main(int argc, char **argv) {
         if (only && !strstr(v.name, only)) continue;
         uint32_t lds_bytes;
         if (v.slice == 1) {
-            mcrc::build_lds_image1(img.data(), v.ch, v.lpi);
+            mcrc::build_lds_image1(img.data(), v.ch);
             lds_bytes = mcrc_dev::kLdsImage1Bytes;
         } else {
-            mcrc::build_lds_image4(img.data(), v.ch, v.lpi);
+            mcrc::build_lds_image4(img.data(), v.ch);
             lds_bytes = mcrc_dev::kLdsImage4Bytes;
         }
         CK(hipMemcpy(d_img, img.data(), lds_bytes, hipMemcpyHostToDevice));
