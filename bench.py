@@ -149,6 +149,108 @@ def cpu_baseline(data: torch.Tensor, out: torch.Tensor):
             "gpu_match": bool((gpu == crc).all())}
 
 
+def zipf_lens(n: int, seed: int = 7):
+    """BASELINE config 3 sizes: 44 classes 64 * 1.25^k <= 1 MiB, Zipf s = 1 over
+    class rank (rank 1 = smallest), length uniform within +-half a class step."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    classes = 64 * 1.25 ** np.arange(44)
+    classes = classes[classes <= 1 << 20]
+    p = 1.0 / np.arange(1, classes.size + 1)
+    k = rng.choice(classes.size, n, p=p / p.sum())
+    step = classes[k] * 0.125
+    return np.clip(classes[k] + rng.uniform(-step, step), 1, 1 << 20).astype(np.uint32)
+
+
+def workload_config3(args, rank, world):
+    """1 Mi spans of Zipf sizes packed back to back at odd offsets (K2)."""
+    import numpy as np
+    lens = zipf_lens(args.items)
+    offs = np.concatenate([[1], 1 + np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    total = int(offs[-1] + lens[-1] + 16)
+    g = torch.Generator(device="cuda").manual_seed(3 + rank)
+    data = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda", generator=g)
+    d_offs = torch.from_numpy(offs.view(np.int64)).cuda()
+    d_lens = torch.from_numpy(lens.view(np.int32)).cuda()
+    out = torch.empty(lens.size, dtype=torch.int32, device="cuda")
+    spans = _lib.Spans(data.data_ptr(), total, d_offs.data_ptr(), 0, d_lens.data_ptr(), 0, None, out.data_ptr(),
+                       lens.size)
+    return spans, int(lens.astype(np.uint64).sum()), {
+        "workload": "BASELINE configs[2]: 1 Mi spans, Zipf sizes 64 B - 1 MiB (44 classes, s = 1), packed "
+                    "back to back at odd offsets, K2 k_spans<unaligned>",
+        "items_per_gpu": int(lens.size), "span_bytes_per_gpu": int(lens.astype(np.uint64).sum()),
+        "items_le_4k_frac": round(float((lens <= 4096).mean()), 3)}
+
+
+def run_verify_steps(args_v, steps: int, stream):
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    base, size, offs, n, ok = args_v
+    nbad = ctypes.c_uint64(0)
+    for a, b in evs:
+        a.record(stream)
+        _lib.check(_lib.lib.crc32c_verify_items(base, size, offs, n, ok, ctypes.byref(nbad), _lib.CRC32C_DEVICE,
+                                                ctypes.c_void_p(stream.cuda_stream)))
+        b.record(stream)
+    return evs, int(nbad.value)
+
+
+def workload_config5(args, rank, world):
+    """Extstore pages of packed 4165-byte item images, stored CRCs verified (K3).
+
+    Pages: args.pages x 64 MiB, each 16 wbufs of 1007 items (key%07d, 4096-byte
+    value, CAS) and a zero tail; 1 % of items get one flipped bit."""
+    import numpy as np
+    per_wbuf, ntotal, wbuf = 1007, 4165, 4 << 20
+    nwb = args.pages * 16
+    g = torch.Generator(device="cuda").manual_seed(5 + rank)
+    data = torch.randint(0, 256, (nwb * wbuf,), dtype=torch.uint8, device="cuda", generator=g)
+    wb = data.view(nwb, wbuf)
+    wb[:, per_wbuf * ntotal:] = 0
+    items = wb[:, : per_wbuf * ntotal].view(nwb, per_wbuf, ntotal)
+    n = nwb * per_wbuf
+    idx = torch.arange(n, device="cuda", dtype=torch.int64).view(nwb, per_wbuf)
+    hdr = torch.zeros(nwb, per_wbuf, 67, dtype=torch.uint8, device="cuda")
+    le = lambda v, k: torch.stack([(v >> (8 * i)) & 0xFF for i in range(k)], -1).to(torch.uint8)
+    hdr[..., 24:28] = le(idx * 2654435761 & 0xFFFFFFFF, 4)        # time (hash)
+    hdr[..., 32:36] = le(torch.full_like(idx, 4098), 4)            # nbytes (value + CRLF)
+    hdr[..., 36] = 1                                               # refcount
+    hdr[..., 38] = 2                                               # it_flags = ITEM_CAS
+    hdr[..., 40] = 17                                              # slabs_clsid
+    hdr[..., 41] = 10                                              # nkey
+    hdr[..., 48:56] = le(idx + 1, 8)                               # CAS
+    hdr[..., 56:59] = torch.tensor(list(b"key"), dtype=torch.uint8, device="cuda")
+    for d in range(7):                                             # key%07d
+        hdr[..., 65 - d] = (48 + (idx // 10 ** d) % 10).to(torch.uint8)
+    hdr[..., 66] = 0
+    items[..., :67] = hdr
+    items[..., 4163] = 13
+    items[..., 4164] = 10
+    offs = (torch.arange(nwb, device="cuda", dtype=torch.int64)[:, None] * wbuf +
+            torch.arange(per_wbuf, device="cuda", dtype=torch.int64)[None, :] * ntotal).reshape(-1).contiguous()
+    # spill CRCs (storage.c:567) into exptime, computed by the span kernel
+    span_offs = (offs + 32).contiguous()
+    crc = torch.empty(n, dtype=torch.int32, device="cuda")
+    sp = _lib.Spans(data.data_ptr(), data.numel(), span_offs.data_ptr(), 0, None, ntotal - 32, None,
+                    crc.data_ptr(), n)
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp), _lib.CRC32C_DEVICE, None))
+    items[..., 28:32] = crc.view(torch.uint8).view(nwb, per_wbuf, 4)
+    # inject one flipped bit into 1 % of items
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    victims = torch.randperm(n, device="cuda", generator=gen)[: n // 100]
+    pos = offs[victims] + 32 + torch.randint(0, ntotal - 32, (victims.numel(),), device="cuda", generator=gen)
+    bit = torch.randint(0, 8, (victims.numel(),), device="cuda", generator=gen).to(torch.uint8)
+    flat = data.view(-1)
+    flat[pos] ^= (torch.ones_like(bit) << bit)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    return (data.data_ptr(), data.numel(), offs.data_ptr(), n, ok.data_ptr()), ok, victims, \
+        n * (ntotal - 32), {
+            "workload": f"BASELINE configs[4]: {args.pages} x 64 MiB extstore pages, 16 wbufs x 1007 packed "
+                        "4165-B item images each, stored CRC verified per item (K3 k_spans<verify>)",
+            "pages_per_gpu": args.pages, "items_per_gpu": n, "span_bytes_per_gpu": n * (ntotal - 32),
+            "injected_bad": int(victims.numel())}
+
+
 def traffic_per_launch():
     """HBM bytes per K1 launch from the committed rocprofv3 --pmc summary, if any."""
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
@@ -170,7 +272,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--items", type=int, default=ITEMS_PER_GPU, help="items per GPU (default: config 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="config2", choices=["config2", "config3", "config5", "host"],
+                    help="config2 = headline; others are extra measurements (not the bench line)")
+    ap.add_argument("--pages", type=int, default=1000, help="config5: 64 MiB pages per GPU")
     args = ap.parse_args()
+    if args.workload != "config2":
+        return extra_workload(args)
 
     rank, world, local = dist_setup(args.gpus)
     if _lib.lib.crc32c_gpu_count() < 1:
@@ -230,6 +337,56 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def extra_workload(args):
+    """Non-headline measurements; prints one JSON line per run."""
+    rank, world, local = dist_setup(args.gpus)
+    stream = torch.cuda.current_stream()
+    res = {"workload_kind": args.workload, "n_gpus": world, "steps": args.steps}
+    if args.workload == "config3":
+        if args.items == ITEMS_PER_GPU:
+            args.items = 1 << 20
+        spans, nbytes, cfg = workload_config3(args, rank, world)
+        run_steps(spans, max(1, args.warmup), stream)
+        torch.cuda.synchronize()
+        elapsed, evs = timed(lambda k: run_steps(spans, k, stream), args.steps, world)
+        kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        res.update(config=cfg, kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
+                   hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+    elif args.workload == "config5":
+        vargs, ok, victims, nbytes, cfg = workload_config5(args, rank, world)
+        run_verify_steps(vargs, max(1, args.warmup), stream)
+        torch.cuda.synchronize()
+        elapsed, (evs, nbad) = timed(lambda k: run_verify_steps(vargs, k, stream), args.steps, world)
+        kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        bad_idx = torch.nonzero(ok == 0).flatten()
+        exact = bool(nbad == victims.numel() and torch.equal(torch.sort(bad_idx)[0], torch.sort(victims)[0]))
+        res.update(config=cfg, kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
+                   hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), nbad=nbad,
+                   detected_exactly_the_injected_items=exact)
+    else:  # host: pinned host memory -> H2D -> K1/K2 -> D2H through the library's host path
+        import numpy as np
+        n = args.items
+        host = torch.empty(n * ITEM_BYTES, dtype=torch.uint8).pin_memory()
+        g = torch.Generator().manual_seed(11)
+        host.copy_(torch.randint(0, 256, (n * ITEM_BYTES,), dtype=torch.uint8, generator=g))
+        out = np.empty(n, np.uint32)
+        sp = _lib.Spans(host.data_ptr(), host.numel(), None, ITEM_BYTES, None, ITEM_BYTES, None,
+                        out.ctypes.data, n)
+        _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp), 0, None))
+
+        def steps(k):
+            for _ in range(k):
+                _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp), 0, None))
+
+        elapsed, _ = timed(steps, args.steps, world, sync=lambda: None)
+        res.update(config={"workload": f"{n} x {ITEM_BYTES} B items in pinned host memory; H2D over PCIe, "
+                                       "K2 kernel, CRCs D2H (library host path, two pipeline slots)"},
+                   gib_s=round(n * ITEM_BYTES * args.steps * world / elapsed / 2**30, 2),
+                   gb_s=round(n * ITEM_BYTES * args.steps * world / elapsed / 1e9, 2))
+    if rank == 0:
+        print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -168,7 +168,8 @@ bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t st) {
     if (s.n == 0) return CRC32C_OK;
     const bool fixed = s.offsets == nullptr && s.lens == nullptr;
-    const uint32_t kspan = fixed ? mcrc::xpow8n(s.len) : 0u;
+    // every span has the same length whenever lens is absent (with or without offsets)
+    const uint32_t kspan = s.lens == nullptr ? mcrc::xpow8n(s.len) : 0u;
     if (fixed && s.len == kFixedLen && aligned16(s.base) && (s.stride & 15u) == 0) {
         const uint32_t kfinal = ~mcrc::Gf2Op::zeros(s.len).apply(0xffffffffu);
         hipLaunchKernelGGL((K1_KERNEL), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImage4Bytes, st,

@@ -133,6 +133,29 @@ def test_realistic_item_spans_4133(torch):
     np.testing.assert_array_equal(_u32(out), want)
 
 
+def test_offsets_with_fixed_length(torch):
+    """offsets[] given, lens[] absent: every span is `len` bytes (config 5 shape)."""
+    import ctypes
+    rng = np.random.default_rng(21)
+    n, L = 1500, 4133
+    offs = (np.arange(n, dtype=np.uint64) * 4165 + 32).astype(np.uint64)
+    host = rng.integers(0, 256, n * 4165 + 64, dtype=np.uint8)
+    cin = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    d, doffs = _dev(torch, host), _dev(torch, offs.view(np.int64))
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    for crc_in in (None, _dev(torch, cin.view(np.int32))):
+        s = _lib.Spans(d.data_ptr(), host.size, doffs.data_ptr(), 0, None, L,
+                       None if crc_in is None else crc_in.data_ptr(), out.data_ptr(), n)
+        _lib.check(_lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None))
+        want = oracle.batch(host, offs, np.full(n, L), None if crc_in is None else cin)
+        np.testing.assert_array_equal(_u32(out), want)
+    # and the host path with the same descriptor shape
+    outh = np.empty(n, np.uint32)
+    s = _lib.Spans(host.ctypes.data, host.size, offs.ctypes.data, 0, None, L, None, outh.ctypes.data, n)
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(s), 0, None))
+    np.testing.assert_array_equal(outh, oracle.batch(host, offs, np.full(n, L)))
+
+
 @pytest.mark.parametrize("name", ["cfg1", "varied"])
 def test_verify_golden_items(torch, name):
     g = np.load(os.path.join(GOLD, "items.npz"))
