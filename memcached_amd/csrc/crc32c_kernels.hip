@@ -252,17 +252,25 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 }
 
 // ===========================================================================
-// K2/K3: arbitrary spans, one 32-lane group per span
+// K2/K3: arbitrary spans, one 32-lane group per work unit
 // ===========================================================================
 //
-// Geometry (CH = 64, LPI = 32): a span [p, E) is covered by npairs row pairs
-// anchored at its END: pair k covers [G + 4096k, G + 4096(k+1)) with
+// Work units.  A span longer than kSegBytes is cut into segments of kSegBytes
+// anchored at its END (segment 0, the head, holds the remainder); every
+// segment is one work unit, so no group owns more than 64 KiB and a batch of
+// Zipf-sized items balances over the grid.  Units come from k_count ->
+// exclusive scan -> k_expand; a batch whose spans are all <= kSegBytes uses
+// unit u = span u directly.  k_combine folds the segment CRCs of long spans:
+//   raw(span) = sum_s M_{64 KiB * (nseg-1-s)}(raw(segment s))   (Horner)
+//
+// Unit geometry (CH = 64, LPI = 32): a unit [p, E) is covered by npairs row
+// pairs anchored at E: pair k covers [G + 4096k, G + 4096(k+1)) with
 // G = E - 4096 * npairs, row A = first 2048 bytes, row B = second.  Lane li
 // owns bytes [64 li, 64 li + 64) of each row.  Bytes before p are zero, which
 // leaves a zero-initialised register unchanged, so the grid needs no tail
 // handling and every lane chain ends on a row boundary.  Per pair a lane folds
 //   acc = M_4096(acc) ^ M_2048(raw A chunk) ^ raw B chunk,
-// and the 32 lane accumulators are merged by group_reduce (levels M_64..M_1024).
+// and the 32 lane accumulators are merged by the lane-group reduction.
 //
 // Loads are always 16-B aligned pieces that overlap [p, E) (so they never leave
 // the pages holding the span); a piece wholly outside is read from a zeroed
@@ -272,6 +280,8 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 constexpr uint32_t kSpanCH = 64;
 constexpr uint32_t kRowBytes = 32 * kSpanCH;  // 2048
 constexpr uint32_t kPairBytes = 2 * kRowBytes;
+constexpr uint32_t kSegBytes = 64 * 1024;
+constexpr uint32_t kWhole = 0xffffffffu;      // unit segment index: the whole span
 
 struct SpanArgs {
     const uint8_t *base;       // all spans live in [base, base + base_bytes)
@@ -286,18 +296,20 @@ struct SpanArgs {
     uint32_t *out;             // MODE 0: CRC per span
     uint8_t *ok;               // MODE 1: 1 if the stored CRC matches
     unsigned long long *nbad;  // MODE 1: count of mismatches (atomic)
-    uint64_t n;
+    uint64_t n;                // spans (items)
     const uint32_t *xpow;      // 3 x 1024 table: x^(8*j), x^(8*1024*j), x^(8*2^20*j)
     const uint4 *zero;         // 16 zero bytes in device memory
+    // work units (nullptr: unit u = span u, one segment)
+    const uint2 *units;        // (span index, segment index or kWhole)
+    const uint32_t *nunits;    // device-side unit count
+    uint32_t *seg_raw;         // raw CRC of each unit of a multi-segment span
 };
 
-struct SpanDesc {
-    const uint8_t *p;  // first byte
+struct ItemDesc {
+    const uint8_t *p;
     uint32_t len;
-    uint32_t aux;      // MODE 0: initial CRC; MODE 1: stored CRC
-    uint32_t npairs;
-    bool valid;        // a span is assigned
-    bool sane;         // MODE 1: header parsed to an in-bounds span
+    uint32_t aux;  // MODE 0: initial CRC; MODE 1: stored CRC
+    bool sane;     // MODE 1: header parsed to an in-bounds span
 };
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
@@ -305,33 +317,81 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t *p) {
     return ld_u8(p) | (ld_u8(p + 1) << 8) | (ld_u8(p + 2) << 16) | (ld_u8(p + 3) << 24);
 }
 
+__device__ __forceinline__ uint32_t nseg_of(uint32_t len) {
+    return len <= kSegBytes ? 1u : (len + kSegBytes - 1) / kSegBytes;
+}
+
 template <int MODE>
-__device__ __forceinline__ SpanDesc fetch_desc(const SpanArgs &a, uint64_t i) {
-    SpanDesc d;
-    d.valid = i < a.n;
-    d.sane = true;
+__device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
+    ItemDesc d;
+    const uint64_t off = a.offsets ? a.offsets[i] : i * a.stride;
+    if (MODE == 0) {
+        d.p = a.base + off;
+        d.len = a.lens ? a.lens[i] : a.len;
+        d.aux = a.crc_in ? a.crc_in[i] : 0u;
+        d.sane = true;
+    } else {
+        // item header fields (memcached.h:613-636), ITEM_ntotal (:149-152)
+        const uint8_t *it = a.base + off;
+        const bool hdr_ok = off + 48 <= a.base_bytes;
+        const uint32_t nbytes = hdr_ok ? ld_u32_unaligned(it + 32) : 0u;
+        const uint32_t flags = hdr_ok ? (ld_u8(it + 38) | (ld_u8(it + 39) << 8)) : 0u;
+        const uint32_t nkey = hdr_ok ? ld_u8(it + 41) : 0u;
+        const uint64_t ntotal = 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) + ((flags & 2u) ? 8 : 0);
+        d.aux = hdr_ok ? ld_u32_unaligned(it + 28) : 0u;
+        d.sane = hdr_ok && nkey != 0 && nbytes < 0x80000000u && off + ntotal <= a.base_bytes;
+        d.p = it + 32;
+        d.len = d.sane ? (uint32_t)(ntotal - 32) : 0u;
+    }
+    return d;
+}
+
+struct UnitDesc {
+    const uint8_t *p;  // first byte of this unit
+    uint32_t len;      // bytes of this unit
+    uint32_t npairs;
+    uint32_t aux;      // of the span
+    uint32_t span_len;
+    uint64_t item;     // span index
+    uint64_t unit;
+    bool valid;
+    bool single;       // the unit is the whole span: finalise directly
+    bool sane;
+};
+
+template <int MODE>
+__device__ __forceinline__ UnitDesc fetch_unit(const SpanArgs &a, uint64_t u, uint64_t nunits) {
+    UnitDesc d;
+    d.valid = u < nunits;
+    d.p = a.base;
     d.len = 0;
     d.aux = 0;
-    d.p = a.base;
+    d.span_len = 0;
+    d.item = 0;
+    d.unit = u;
+    d.single = true;
+    d.sane = true;
     if (d.valid) {
-        const uint64_t off = a.offsets ? a.offsets[i] : i * a.stride;
-        if (MODE == 0) {
-            d.p = a.base + off;
-            d.len = a.lens ? a.lens[i] : a.len;
-            d.aux = a.crc_in ? a.crc_in[i] : 0u;
+        uint32_t seg = kWhole;  // without a unit list every span is one unit
+        d.item = u;
+        if (a.units) {
+            const uint2 e = a.units[u];
+            d.item = e.x;
+            seg = e.y;
+        }
+        const ItemDesc it = fetch_item<MODE>(a, d.item);
+        d.aux = it.aux;
+        d.span_len = it.len;
+        d.sane = it.sane;
+        const uint32_t nseg = seg == kWhole ? 1u : nseg_of(it.len);
+        d.single = nseg == 1;
+        if (d.single) {
+            d.p = it.p;
+            d.len = it.len;
         } else {
-            // item header fields (memcached.h:613-636), ITEM_ntotal (:149-152)
-            const uint8_t *it = a.base + off;
-            const bool hdr_ok = off + 48 <= a.base_bytes;
-            const uint32_t nbytes = hdr_ok ? ld_u32_unaligned(it + 32) : 0u;
-            const uint32_t flags = hdr_ok ? (ld_u8(it + 38) | (ld_u8(it + 39) << 8)) : 0u;
-            const uint32_t nkey = hdr_ok ? ld_u8(it + 41) : 0u;
-            const uint64_t ntotal = 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) +
-                                    ((flags & 2u) ? 8 : 0);
-            d.aux = hdr_ok ? ld_u32_unaligned(it + 28) : 0u;
-            d.sane = hdr_ok && nkey != 0 && nbytes < 0x80000000u && off + ntotal <= a.base_bytes;
-            d.p = it + 32;
-            d.len = d.sane ? (uint32_t)(ntotal - 32) : 0u;
+            const uint8_t *seg_end = it.p + it.len - (size_t)(nseg - 1 - seg) * kSegBytes;
+            d.p = seg == 0 ? it.p : seg_end - kSegBytes;
+            d.len = (uint32_t)(seg_end - d.p);
         }
     }
     d.npairs = (d.len + kPairBytes - 1) / kPairBytes;
@@ -349,10 +409,10 @@ struct PairWin {
     RowWin<UNALIGNED> a, b;
 };
 
-// Issue the loads of row pair k of span d for lane li.
+// Issue the loads of row pair k of unit d for lane li.
 template <bool UNALIGNED>
-__device__ __forceinline__ void load_pair(PairWin<UNALIGNED> &w, const SpanDesc &d, uint32_t k,
-                                          uint32_t li, const uint4 *zero) {
+__device__ __forceinline__ void load_pair(PairWin<UNALIGNED> &w, const UnitDesc &d, uint32_t k, uint32_t li,
+                                          const uint4 *zero) {
     const uint8_t *E = d.p + d.len;
     const uint8_t *G = E - (size_t)kPairBytes * d.npairs + (size_t)kPairBytes * k;
     const uint8_t *sa = G + kSpanCH * li;
@@ -369,15 +429,11 @@ __device__ __forceinline__ void load_pair(PairWin<UNALIGNED> &w, const SpanDesc 
     }
 }
 
-__device__ __forceinline__ uint32_t dw(const uint4 &v, int k) {
-    return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
-}
-
 // Realign a five-piece window to the 16 chunk dwords starting at byte u.
 __device__ __forceinline__ void realign(const RowWin<true> &w, uint32_t u, uint32_t out[16]) {
     uint32_t t[20];
 #pragma unroll
-    for (int i = 0; i < 20; ++i) t[i] = dw(w.v[i >> 2], i & 3);
+    for (int i = 0; i < 20; ++i) t[i] = dw4(w.v[i >> 2], i & 3);
     const bool q2 = u & 8u, q1 = u & 4u;
 #pragma unroll
     for (int i = 0; i < 18; ++i) t[i] = q2 ? t[i + 2] : t[i];
@@ -390,10 +446,10 @@ __device__ __forceinline__ void realign(const RowWin<true> &w, uint32_t u, uint3
 
 __device__ __forceinline__ void straight(const RowWin<false> &w, uint32_t out[16]) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) out[i] = dw(w.v[i >> 2], i & 3);
+    for (int i = 0; i < 16; ++i) out[i] = dw4(w.v[i >> 2], i & 3);
 }
 
-// Zero the chunk bytes that precede the span start p (lo = p - chunk start).
+// Zero the chunk bytes that precede the unit start p (lo = p - chunk start).
 __device__ __forceinline__ void mask_head(uint32_t v[16], int64_t lo) {
     const int32_t l = lo < 0 ? 0 : lo > 64 ? 64 : (int32_t)lo;
 #pragma unroll
@@ -404,14 +460,15 @@ __device__ __forceinline__ void mask_head(uint32_t v[16], int64_t lo) {
     }
 }
 
-// Two independent chains (rows A and B) from zero registers, interleaved.
+// Two independent chains (rows A and B) from zero registers, interleaved,
+// with bitop3-fused XORs.
 __device__ __forceinline__ void chain16x2(const uint32_t a[16], const uint32_t b[16], const LaneCtx &c,
                                           uint32_t &sa, uint32_t &sb) {
-    uint32_t x = 0, y = 0;
+    uint32_t x = a[0], y = b[0];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        x = Step<4>::dword(x ^ a[i], c);
-        y = Step<4>::dword(y ^ b[i], c);
+        x = step4_next(x, i + 1 < 16 ? a[i + 1] : 0u, c);
+        y = step4_next(y, i + 1 < 16 ? b[i + 1] : 0u, c);
     }
     sa = x;
     sb = y;
@@ -425,6 +482,25 @@ __device__ __forceinline__ uint32_t xpow8_dev(const uint32_t *xp, uint32_t len) 
     return r;
 }
 
+// crc32c(c, D) = ~(M_len(~c) ^ raw(D)), then store (MODE 0) or compare (MODE 1).
+template <int MODE>
+__device__ __forceinline__ void finalize(const SpanArgs &a, uint64_t item, uint32_t raw, uint32_t aux,
+                                         uint32_t span_len, bool sane) {
+    uint32_t init;
+    if (MODE == 0 && a.lens == nullptr)
+        init = mulmodp_dev(~aux, a.kspan);
+    else
+        init = mulmodp_dev(MODE == 0 ? ~aux : 0xffffffffu, xpow8_dev(a.xpow, span_len));
+    const uint32_t crc = ~(init ^ raw);
+    if (MODE == 0) {
+        a.out[item] = crc;
+    } else {
+        const bool good = sane && crc == aux;
+        a.ok[item] = good;
+        if (!good) atomicAdd(a.nbad, 1ull);
+    }
+}
+
 template <bool UNALIGNED, int MODE>
 __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restrict__ img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -434,18 +510,19 @@ __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restr
     LaneCtx c;
     c.lane4 = li << 2;
     c.lane4hi = c.lane4 | 0x10000u;
+    const uint64_t nunits = a.units ? (uint64_t)*a.nunits : a.n;
     const uint64_t ngroups_total = (uint64_t)gridDim.x * (blockDim.x >> 5);
-    uint64_t it = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+    uint64_t u = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
 
-    SpanDesc cur = fetch_desc<MODE>(a, it);
-    SpanDesc nxt = fetch_desc<MODE>(a, it + ngroups_total);
+    UnitDesc cur = fetch_unit<MODE>(a, u, nunits);
+    UnitDesc nxt = fetch_unit<MODE>(a, u + ngroups_total, nunits);
     uint32_t k = 0;    // pair index inside cur
     uint32_t acc = 0;  // lane accumulator over the pairs of cur
     PairWin<UNALIGNED> w0, w1;
     load_pair<UNALIGNED>(w0, cur, 0, li, a.zero);
 
     // Process the pair held in `w` (pair k of cur) after issuing the loads of
-    // the group's next unit into `wn`.  Returns false once this group is done.
+    // the group's next pair into `wn`.  Returns false once this group is done.
     auto step = [&](PairWin<UNALIGNED> &w, PairWin<UNALIGNED> &wn) -> bool {
         const bool last = k + 1 >= cur.npairs;
         if (!last)
@@ -456,12 +533,11 @@ __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restr
         if (cur.npairs) {
             uint32_t va[16], vb[16];
             const uint8_t *E = cur.p + cur.len;
-            const uint8_t *sa =
-                E - (size_t)kPairBytes * cur.npairs + (size_t)kPairBytes * k + kSpanCH * li;
+            const uint8_t *sa = E - (size_t)kPairBytes * cur.npairs + (size_t)kPairBytes * k + kSpanCH * li;
             if constexpr (UNALIGNED) {
-                const uint32_t u = (uint32_t)((uintptr_t)E & 15u);
-                realign(w.a, u, va);
-                realign(w.b, u, vb);
+                const uint32_t uo = (uint32_t)((uintptr_t)E & 15u);
+                realign(w.a, uo, va);
+                realign(w.b, uo, vb);
             } else {
                 straight(w.a, va);
                 straight(w.b, vb);
@@ -474,33 +550,23 @@ __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restr
             }
             uint32_t s_a, s_b;
             chain16x2(va, vb, c, s_a, s_b);
-            acc = apply_op<4>(kAuxOp6, acc) ^ apply_op<4>(kAuxOp5, s_a) ^ s_b;
+            acc = xor3(apply_op<4>(kAuxOp6, acc), apply_op<4>(kAuxOp5, s_a), s_b);
         }
         if (last) {
             if (cur.valid) {
-                const uint32_t raw = group_reduce<4, 32>(acc, lane);
+                const uint32_t raw = group_reduce32_dpp(acc, lane);
                 if (li == 0) {
-                    // crc32c(c, D) = ~(M_len(~c) ^ raw(D))
-                    uint32_t init;
-                    if (a.lens == nullptr && MODE == 0)
-                        init = mulmodp_dev(~cur.aux, a.kspan);
+                    if (cur.single)
+                        finalize<MODE>(a, cur.item, raw, cur.aux, cur.span_len, cur.sane);
                     else
-                        init = mulmodp_dev(MODE == 0 ? ~cur.aux : 0xffffffffu, xpow8_dev(a.xpow, cur.len));
-                    const uint32_t crc = ~(init ^ raw);
-                    if (MODE == 0) {
-                        a.out[it] = crc;
-                    } else {
-                        const bool good = cur.sane && crc == cur.aux;
-                        a.ok[it] = good;
-                        if (!good) atomicAdd(a.nbad, 1ull);
-                    }
+                        a.seg_raw[cur.unit] = raw;
                 }
             }
             acc = 0;
             k = 0;
-            it += ngroups_total;
+            u += ngroups_total;
             cur = nxt;
-            nxt = fetch_desc<MODE>(a, it + ngroups_total);
+            nxt = fetch_unit<MODE>(a, u + ngroups_total, nunits);
         } else {
             ++k;
         }
@@ -510,6 +576,49 @@ __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restr
     for (;;) {
         if (!step(w0, w1)) break;
         if (!step(w1, w0)) break;
+    }
+}
+
+// Segments per span (for the exclusive scan that places the work units).
+template <int MODE>
+__global__ void k_count(SpanArgs a, uint32_t *nseg) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        nseg[i] = nseg_of(fetch_item<MODE>(a, i).len);
+}
+
+// Write unit descriptors at prefix[i].  Spans whose units would pass `cap`
+// (possible only when spans overlap) are listed in `whole` and processed as
+// one unit each by a second pass; *nvalid = units written before the first
+// such span.
+__global__ void k_expand(const uint32_t *nseg, const uint32_t *prefix, uint64_t n, uint2 *units, uint64_t cap,
+                         uint32_t *nvalid, uint2 *whole, uint32_t *nwhole) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p0 = prefix[i], ns = nseg[i];
+        if (p0 + ns <= cap) {
+            for (uint32_t s = 0; s < ns; ++s) units[p0 + s] = make_uint2((uint32_t)i, s);
+            if (i + 1 == n) *nvalid = (uint32_t)(p0 + ns);
+        } else {
+            if (p0 <= cap) atomicMin(nvalid, (uint32_t)p0);
+            whole[atomicAdd(nwhole, 1u)] = make_uint2((uint32_t)i, kWhole);
+        }
+    }
+}
+
+// Fold the segment CRCs of every multi-segment span (one thread per span).
+template <int MODE>
+__global__ void k_combine(SpanArgs a, const uint32_t *nseg, const uint32_t *prefix, const uint32_t *nvalid,
+                          uint32_t kseg) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t ns = nseg[i];
+        const uint64_t p0 = prefix[i];
+        if (ns <= 1 || p0 + ns > *nvalid) continue;  // single, or processed whole
+        uint32_t acc = 0;
+        for (uint32_t s = 0; s < ns; ++s) acc = mulmodp_dev(acc, kseg) ^ a.seg_raw[p0 + s];
+        const ItemDesc it = fetch_item<MODE>(a, i);
+        finalize<MODE>(a, i, acc, it.aux, it.len, it.sane);
     }
 }
 

@@ -5,6 +5,7 @@
 // (crc32c.c:47, :266-275, :507-513); the batch symbols replace loops of those
 // calls in storage.c / proxy_internal.c (see include/crc32c_batch.h).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -77,6 +78,12 @@ struct Device {
     uint64_t *hoffs[2] = {nullptr, nullptr};  // pinned twins of the descriptor slots
     uint32_t *hlens[2] = {nullptr, nullptr}, *hcin[2] = {nullptr, nullptr}, *hout[2] = {nullptr, nullptr};
     uint64_t slot_items = 0;
+    // work-unit planning for long / variable spans (grow-only)
+    uint32_t *nseg = nullptr, *prefix = nullptr, *seg_raw = nullptr, *counters = nullptr;
+    uint2 *units = nullptr, *whole = nullptr;
+    void *scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
+    uint64_t plan_items = 0, plan_units = 0;
 };
 
 std::mutex g_dev_mu;
@@ -164,7 +171,83 @@ int grid_for(const Device &d, uint64_t n) {
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
-// Enqueue the kernel for a device-resident batch on `st`.
+int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
+    if (d.plan_items < n) {
+        (void)hipFree(d.nseg);
+        (void)hipFree(d.prefix);
+        (void)hipFree(d.whole);
+        d.plan_items = 0;
+        if (hipMalloc(&d.nseg, n * 4) != hipSuccess || hipMalloc(&d.prefix, n * 4) != hipSuccess ||
+            hipMalloc(&d.whole, n * 8) != hipSuccess)
+            return CRC32C_ENOMEM;
+        size_t need = 0;
+        if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, d.nseg, d.prefix, (int)n) != hipSuccess)
+            return CRC32C_EHIP;
+        if (need > d.scan_tmp_bytes) {
+            (void)hipFree(d.scan_tmp);
+            if (hipMalloc(&d.scan_tmp, need) != hipSuccess) return CRC32C_ENOMEM;
+            d.scan_tmp_bytes = need;
+        }
+        d.plan_items = n;
+    }
+    if (d.plan_units < cap) {
+        (void)hipFree(d.units);
+        (void)hipFree(d.seg_raw);
+        d.plan_units = 0;
+        if (hipMalloc(&d.units, cap * 8) != hipSuccess || hipMalloc(&d.seg_raw, cap * 4) != hipSuccess)
+            return CRC32C_ENOMEM;
+        d.plan_units = cap;
+    }
+    if (!d.counters && hipMalloc(&d.counters, 16) != hipSuccess) return CRC32C_ENOMEM;
+    return CRC32C_OK;
+}
+
+template <int MODE>
+int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) {
+    const uint64_t n = a.n;
+    const bool identity = MODE == 0 && a.lens == nullptr && a.len <= mcrc_dev::kSegBytes;
+    auto spans = [&](const mcrc_dev::SpanArgs &x, int grid) {
+        if (aligned && MODE == 0)
+            hipLaunchKernelGGL((mcrc_dev::k_spans<false, MODE>), dim3(grid), dim3(kBlock),
+                               mcrc_dev::kLdsImage4Bytes, st, x, d.img);
+        else
+            hipLaunchKernelGGL((mcrc_dev::k_spans<true, MODE>), dim3(grid), dim3(kBlock),
+                               mcrc_dev::kLdsImage4Bytes, st, x, d.img);
+    };
+    if (identity) {
+        spans(a, grid_for(d, n));
+        return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
+    }
+    if (n >= 0xffffffffull) return CRC32C_EINVAL;
+    // units fit in cap whenever the spans do not overlap; overlapping long spans
+    // past cap are processed whole by the second span pass
+    const uint64_t cap = std::min<uint64_t>(n + a.base_bytes / mcrc_dev::kSegBytes + 1, 0xfffffff0ull);
+    int rc = ensure_plan(d, n, cap);
+    if (rc) return rc;
+    uint32_t *nvalid = d.counters, *nwhole = d.counters + 1;
+    const int g1 = (int)std::min<uint64_t>((n + 255) / 256, 4096);
+    HIP_OK(hipMemsetAsync(nvalid, 0xff, 4, st));
+    HIP_OK(hipMemsetAsync(nwhole, 0, 4, st));
+    hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nseg);
+    size_t tmp = d.scan_tmp_bytes;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(d.scan_tmp, tmp, d.nseg, d.prefix, (int)n, st));
+    hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(g1), dim3(256), 0, st, d.nseg, d.prefix, n, d.units, cap, nvalid,
+                       d.whole, nwhole);
+    mcrc_dev::SpanArgs u = a;
+    u.units = d.units;
+    u.nunits = nvalid;
+    u.seg_raw = d.seg_raw;
+    spans(u, d.cus);
+    mcrc_dev::SpanArgs w = a;
+    w.units = d.whole;
+    w.nunits = nwhole;
+    spans(w, d.cus);
+    hipLaunchKernelGGL((mcrc_dev::k_combine<MODE>), dim3(g1), dim3(256), 0, st, u, d.nseg, d.prefix, nvalid,
+                       mcrc::xpow8n(mcrc_dev::kSegBytes));
+    return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
+}
+
+// Enqueue the kernels for a device-resident batch on `st`.
 int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t st) {
     if (s.n == 0) return CRC32C_OK;
     const bool fixed = s.offsets == nullptr && s.lens == nullptr;
@@ -174,30 +257,24 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
         const uint32_t kfinal = ~mcrc::Gf2Op::zeros(s.len).apply(0xffffffffu);
         hipLaunchKernelGGL((K1_KERNEL), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImage4Bytes, st,
                            (const uint8_t *)s.base, s.stride, s.n, d.img_k1, kfinal, kspan, s.crc_in, s.out);
-    } else {
-        mcrc_dev::SpanArgs a{};
-        a.base = (const uint8_t *)s.base;
-        a.base_bytes = s.base_bytes;
-        a.offsets = s.offsets;
-        a.stride = s.stride;
-        a.lens = s.lens;
-        a.len = s.len;
-        a.kspan = kspan;
-        a.crc_in = s.crc_in;
-        a.out = s.out;
-        a.n = s.n;
-        a.xpow = d.xpow;
-        a.zero = d.zero;
-        const bool aligned = (flags & CRC32C_ALIGNED16) ||
-                             (fixed && aligned16(s.base) && (s.stride & 15u) == 0 && (s.len & 15u) == 0);
-        if (aligned)
-            hipLaunchKernelGGL((mcrc_dev::k_spans<false, 0>), dim3(grid_for(d, s.n)), dim3(kBlock),
-                               mcrc_dev::kLdsImage4Bytes, st, a, d.img);
-        else
-            hipLaunchKernelGGL((mcrc_dev::k_spans<true, 0>), dim3(grid_for(d, s.n)), dim3(kBlock),
-                               mcrc_dev::kLdsImage4Bytes, st, a, d.img);
+        return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
     }
-    return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
+    mcrc_dev::SpanArgs a{};
+    a.base = (const uint8_t *)s.base;
+    a.base_bytes = s.base_bytes;
+    a.offsets = s.offsets;
+    a.stride = s.stride;
+    a.lens = s.lens;
+    a.len = s.len;
+    a.kspan = kspan;
+    a.crc_in = s.crc_in;
+    a.out = s.out;
+    a.n = s.n;
+    a.xpow = d.xpow;
+    a.zero = d.zero;
+    const bool aligned = (flags & CRC32C_ALIGNED16) ||
+                         (fixed && aligned16(s.base) && (s.stride & 15u) == 0 && (s.len & 15u) == 0);
+    return launch_units<0>(d, a, aligned, st);
 }
 
 bool is_pinned_or_device(const void *p) {
@@ -434,11 +511,13 @@ int crc32c_verify_items(const void *base, uint64_t base_bytes, const uint64_t *i
     a.xpow = d->xpow;
     a.zero = d->zero;
     (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
-    hipLaunchKernelGGL((mcrc_dev::k_spans<true, 1>), dim3(grid_for(*d, n)), dim3(kBlock),
-                       mcrc_dev::kLdsImage4Bytes, st, a, d->img);
+    rc = launch_units<1>(*d, a, false, st);
+    if (rc) {
+        cleanup();
+        return rc;
+    }
     unsigned long long bad = 0;
-    bool fail = hipGetLastError() != hipSuccess;
-    fail = fail || hipMemcpyAsync(&bad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st) != hipSuccess;
+    bool fail = hipMemcpyAsync(&bad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st) != hipSuccess;
     if (!dev) fail = fail || hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, st) != hipSuccess;
     fail = fail || hipStreamSynchronize(st) != hipSuccess;
     cleanup();

@@ -119,6 +119,55 @@ def test_variable_unaligned_up_to_1mib(torch):
     np.testing.assert_array_equal(mc.batch_multi(host, offsets=offs, lens=lens, crc_in=cin), want)
 
 
+@pytest.mark.parametrize("aligned", [False, True])
+def test_long_spans_cross_segments(torch, aligned):
+    """Spans of several 64 KiB work units: segment split + combine pass."""
+    rng = np.random.default_rng(31 + aligned)
+    lens = rng.integers(0, 5 << 20, 60).astype(np.uint32)
+    lens[:6] = [65536, 65537, 65535, 131072, 131073, (3 << 20) + 5]
+    if aligned:
+        lens = (lens // 16 * 16).astype(np.uint32)
+    pad = 16 if aligned else 7
+    offs = np.concatenate([[pad], pad + np.cumsum(lens[:-1].astype(np.uint64) + pad)]).astype(np.uint64)
+    host = rng.integers(0, 256, int(offs[-1] + lens[-1] + 64), dtype=np.uint8)
+    cin = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(host, offs, lens, cin)
+    d = _dev(torch, host)
+    out = mc.batch(d, offsets=_dev(torch, offs.view(np.int64)), lens=_dev(torch, lens.view(np.int32)),
+                   crc_in=_dev(torch, cin.view(np.int32)), aligned16=aligned)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), want)
+
+
+def test_overlapping_long_spans_whole_pass(torch):
+    """Overlapping spans whose units exceed the planner's capacity are processed
+    whole by the second pass; results stay exact."""
+    rng = np.random.default_rng(33)
+    host = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    n = 300
+    offs = rng.integers(0, 200000, n).astype(np.uint64)
+    lens = rng.integers(70000, (1 << 20) - 200000, n).astype(np.uint32)
+    want = oracle.batch(host, offs, lens)
+    out = mc.batch(_dev(torch, host), offsets=_dev(torch, offs.view(np.int64)), lens=_dev(torch, lens.view(np.int32)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), want)
+
+
+def test_verify_long_items(torch):
+    """Page verify of items whose spans exceed one 64 KiB unit."""
+    rng = np.random.default_rng(35)
+    items = [layout.make_item(b"big%05d" % i, rng.integers(0, 256, int(rng.integers(60000, 300000)),
+                                                           dtype=np.uint8).tobytes(), cas=i) for i in range(40)]
+    buf, offs = layout.pack_wbufs(items, 1 << 20)
+    soffs, slens = layout.spans_of(buf, offs)
+    layout.store_crcs(buf, offs, oracle.batch(buf, soffs, slens))
+    ok, nbad = mc.verify_items(_dev(torch, buf), _dev(torch, offs.view(np.int64)))
+    assert nbad == 0 and ok.cpu().numpy().all()
+    buf[int(offs[5]) + 70000] ^= 4
+    ok, nbad = mc.verify_items(buf, offs)
+    assert nbad == 1 and ok[5] == 0
+
+
 def test_realistic_item_spans_4133(torch):
     """config-1/config-5 geometry: 4133-byte spans at +32 of 4165-byte images."""
     items = [layout.make_item(b"key%07d" % i, np.random.default_rng(i).integers(0, 256, 4096, dtype=np.uint8).tobytes(),
