@@ -25,7 +25,7 @@
 // operator o occupies aux tables 4o..4o+3:
 //   o = 0..5 : M_{CH * 2^o}  (lane-group reduction level o; for LPI = 32,
 //              o = 5 is M_{32*CH}, the row fold)
-//   o = 6    : M_{2 * 32 * CH} (row-pair fold of the span kernel)
+//   o = 6    : M_{4 * 32 * CH} (4-row block fold of the span kernels)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -35,7 +35,7 @@ namespace mcrc_dev {
 
 constexpr uint32_t kAuxTree = 0;
 constexpr uint32_t kAuxOp5 = 20;  // M_{32*CH}
-constexpr uint32_t kAuxOp6 = 24;  // M_{64*CH}
+constexpr uint32_t kAuxOp6 = 24;  // M_{128*CH}
 constexpr uint32_t kLdsImage1Bytes = 256 * 64 * 4;              // 64 KiB
 constexpr uint32_t kAux4Bytes = 28 * 1024;                        // 28 KiB
 constexpr uint32_t kLdsImage4Bytes = kAux4Bytes + 2 * 65536;     // 156 KiB

@@ -75,6 +75,34 @@ struct Gf2Op {
         }
         return result;
     }
+    // Inverse map (Gauss-Jordan over GF(2)); M_n is invertible because the
+    // polynomial has a constant term, so M_{-n} undoes n zero bytes.
+    Gf2Op inverse() const {
+        uint32_t a[32], b[32];  // rows of the matrix (bit j of row i = column j bit i) and of I
+        for (int i = 0; i < 32; ++i) {
+            a[i] = 0;
+            for (int j = 0; j < 32; ++j) a[i] |= ((col[j] >> i) & 1u) << j;
+            b[i] = 1u << i;
+        }
+        for (int c = 0; c < 32; ++c) {
+            int r = c;
+            while (r < 32 && !((a[r] >> c) & 1u)) ++r;
+            if (r == 32) return identity();  // singular (cannot happen for M_n)
+            uint32_t t = a[r]; a[r] = a[c]; a[c] = t;
+            t = b[r]; b[r] = b[c]; b[c] = t;
+            for (int i = 0; i < 32; ++i)
+                if (i != c && ((a[i] >> c) & 1u)) {
+                    a[i] ^= a[c];
+                    b[i] ^= b[c];
+                }
+        }
+        Gf2Op out;  // b holds the inverse by rows; convert back to columns
+        for (int j = 0; j < 32; ++j) {
+            out.col[j] = 0;
+            for (int i = 0; i < 32; ++i) out.col[j] |= ((b[i] >> j) & 1u) << i;
+        }
+        return out;
+    }
     // Four byte-slice tables so that apply(v) = t[0][v&255] ^ t[1][(v>>8)&255]
     // ^ t[2][(v>>16)&255] ^ t[3][v>>24]  (the form of crc32c.c:121-137).
     void byte_tables(uint32_t t[4][256]) const {
@@ -105,10 +133,14 @@ inline uint32_t xpow8n(uint64_t n) {
     return result;
 }
 
+// x^(-8n) mod P: multiplying a register by it undoes n zero bytes.
+inline uint32_t xpow8n_inv(uint64_t n) { return Gf2Op::zeros(n).inverse().apply(0x80000000u); }
+
 // ---------------------------------------------------------------------------
 // LDS table images for the HIP kernels (layouts documented in crc32c_device.h).
 //   chunk = CH, bytes per lane per row.  Operator o = 0..6 fills aux tables
-//   4o..4o+3: o <= 5 is M_{chunk * 2^o}, o = 6 is M_{64 * chunk}.
+//   4o..4o+3: o <= 5 is M_{chunk * 2^o}, o = 6 is M_{128 * chunk}
+//   (the 4-row block fold of the span kernels).
 // ---------------------------------------------------------------------------
 constexpr int kImage1Dwords = 256 * 64;                    // SLICE 1: 64 KiB
 constexpr int kAux4Dwords = 28 * 256;                      // SLICE 4 aux: 28 KiB
@@ -118,7 +150,7 @@ constexpr int kAuxFold = 24;
 
 inline void aux_ops(uint32_t chunk, Gf2Op ops[7]) {
     for (int k = 0; k < 6; ++k) ops[k] = Gf2Op::zeros((uint64_t)chunk << k);
-    ops[6] = Gf2Op::zeros((uint64_t)chunk * 64);
+    ops[6] = Gf2Op::zeros((uint64_t)chunk * 128);
 }
 
 inline void build_lds_image1(uint32_t *img, uint32_t chunk) {

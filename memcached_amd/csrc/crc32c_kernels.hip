@@ -255,31 +255,41 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 // K2/K3: arbitrary spans, one 32-lane group per work unit
 // ===========================================================================
 //
-// Work units.  A span longer than kSegBytes is cut into segments of kSegBytes
-// anchored at its END (segment 0, the head, holds the remainder); every
-// segment is one work unit, so no group owns more than 64 KiB and a batch of
+// Virtual span.  A span [p, E) is processed as [p, Ea) with Ea = E rounded up
+// to 16: the t = Ea - E bytes after E are zeroed, so the kernel computes
+// raw_v = M_t(raw(D')) and the finalisation multiplies by x^(-8t).  D' is D
+// with ~crc_in XORed into its first four bytes -- exactly what a CRC register
+// initialised to ~crc_in does to them (crc32c.c:166, :397) -- so for
+// |D| >= 4:   crc32c(crc_in, D) = ~M_{-t}(raw_v).
+// Every load is a 16-B aligned piece, and bytes before p are zero.
+//
+// Work units.  A virtual span longer than kSegBytes is cut into segments of
+// kSegBytes anchored at Ea (segment 0, the head, holds the remainder: 17 B to
+// kSegBytes + 16 B); every segment is one work unit, so no group owns much
+// more than 64 KiB and a batch of
 // Zipf-sized items balances over the grid.  Units come from k_count ->
-// exclusive scan -> k_expand; a batch whose spans are all <= kSegBytes uses
-// unit u = span u directly.  k_combine folds the segment CRCs of long spans:
-//   raw(span) = sum_s M_{64 KiB * (nseg-1-s)}(raw(segment s))   (Horner)
+// exclusive scan -> k_expand; a batch whose spans all fit one unit uses unit
+// u = span u directly.  k_combine folds the segment values of long spans:
+//   raw_v(span) = sum_s M_{64 KiB * (nseg-1-s)}(raw_v(segment s))   (Horner)
 //
-// Unit geometry (CH = 64, LPI = 32): a unit [p, E) is covered by npairs row
-// pairs anchored at E: pair k covers [G + 4096k, G + 4096(k+1)) with
-// G = E - 4096 * npairs, row A = first 2048 bytes, row B = second.  Lane li
-// owns bytes [64 li, 64 li + 64) of each row.  Bytes before p are zero, which
-// leaves a zero-initialised register unchanged, so the grid needs no tail
-// handling and every lane chain ends on a row boundary.  Per pair a lane folds
-//   acc = M_4096(acc) ^ M_2048(raw A chunk) ^ raw B chunk,
-// and the 32 lane accumulators are merged by the lane-group reduction.
+// Unit geometry (the K1 geometry: CH = 32, LPI = 32): a unit [p, e), e
+// 16-aligned, is covered by `niters` blocks of 4 KiB anchored at e; block k
+// covers [G + 4096k, G + 4096(k+1)), G = e - 4096 * niters, as four 1 KiB rows.
+// Lane li owns bytes [32 li, 32 li + 32) of every row (two 16-B pieces) and
+// runs one chain per row; rows wholly before p (for every lane of the wave)
+// are skipped.  Per block a lane folds
+//   acc = M_4096(acc) ^ (((s0 M_1024 ^ s1) M_1024 ^ s2) M_1024 ^ s3),
+// and the lane accumulators merge in the K1 lane-group reduction.
 //
-// Loads are always 16-B aligned pieces that overlap [p, E) (so they never leave
-// the pages holding the span); a piece wholly outside is read from a zeroed
-// device buffer instead, so no load is predicated.  When E is not 16-B aligned
-// every lane reads five pieces and realigns them with v_alignbyte.
+// Loads are 16-B aligned pieces that overlap [p, E) (so they never leave the
+// pages holding the span); a piece wholly outside is read from a zeroed device
+// buffer instead, so no load is predicated.  Only two pieces per span hold
+// foreign bytes: the one containing p (masked in the head block) and the last
+// one (bytes >= E; lane 31 / row 3 / piece 1 of the last block).
 
-constexpr uint32_t kSpanCH = 64;
-constexpr uint32_t kRowBytes = 32 * kSpanCH;  // 2048
-constexpr uint32_t kPairBytes = 2 * kRowBytes;
+constexpr uint32_t kSpanCH = 32;
+constexpr uint32_t kRowBytes = 32 * kSpanCH;  // 1024
+constexpr uint32_t kBlockBytes = 4 * kRowBytes;  // 4096
 constexpr uint32_t kSegBytes = 64 * 1024;
 constexpr uint32_t kWhole = 0xffffffffu;      // unit segment index: the whole span
 
@@ -291,18 +301,18 @@ struct SpanArgs {
     uint64_t stride;           // when offsets == nullptr: base + i * stride
     const uint32_t *lens;      // per-span lengths, or nullptr: every span is `len`
     uint32_t len;
-    uint32_t kspan;            // x^(8*len) when lens == nullptr
+    uint32_t kspan16[16];      // lens == nullptr: x^(8*(len+t)) for t = 0..15
     const uint32_t *crc_in;    // MODE 0: per-span initial CRC or nullptr (0)
     uint32_t *out;             // MODE 0: CRC per span
     uint8_t *ok;               // MODE 1: 1 if the stored CRC matches
     unsigned long long *nbad;  // MODE 1: count of mismatches (atomic)
     uint64_t n;                // spans (items)
-    const uint32_t *xpow;      // 3 x 1024 table: x^(8*j), x^(8*1024*j), x^(8*2^20*j)
+    const uint32_t *xpow;      // x^(8*j), x^(8*1024*j), x^(8*2^20*j) (3 x 1024), x^(-8t) (16)
     const uint4 *zero;         // 16 zero bytes in device memory
     // work units (nullptr: unit u = span u, one segment)
     const uint2 *units;        // (span index, segment index or kWhole)
     const uint32_t *nunits;    // device-side unit count
-    uint32_t *seg_raw;         // raw CRC of each unit of a multi-segment span
+    uint32_t *seg_raw;         // raw_v of each unit of a multi-segment span
 };
 
 struct ItemDesc {
@@ -317,8 +327,14 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t *p) {
     return ld_u8(p) | (ld_u8(p + 1) << 8) | (ld_u8(p + 2) << 16) | (ld_u8(p + 3) << 24);
 }
 
-__device__ __forceinline__ uint32_t nseg_of(uint32_t len) {
-    return len <= kSegBytes ? 1u : (len + kSegBytes - 1) / kSegBytes;
+__device__ __forceinline__ uint32_t tail_pad(const uint8_t *p, uint32_t len) {
+    return (uint32_t)(-(uintptr_t)(p + len)) & 15u;
+}
+
+// Segments of a virtual span of vlen bytes.  The head segment keeps more than
+// 16 bytes (up to kSegBytes + 16), so the injected ~crc_in never leaves it.
+__device__ __forceinline__ uint32_t nseg_of(uint32_t vlen) {
+    return vlen <= kSegBytes + 16 ? 1u : (vlen - 16 + kSegBytes - 1) / kSegBytes;
 }
 
 template <int MODE>
@@ -346,132 +362,115 @@ __device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
     return d;
 }
 
+// Descriptor of one work unit, kept compact (two are live per lane).
 struct UnitDesc {
     const uint8_t *p;  // first byte of this unit
-    uint32_t len;      // bytes of this unit
-    uint32_t npairs;
-    uint32_t aux;      // of the span
-    uint32_t span_len;
-    uint64_t item;     // span index
-    uint64_t unit;
-    bool valid;
-    bool single;       // the unit is the whole span: finalise directly
-    bool sane;
+    uint32_t eo;       // e - p: e = 16-aligned end of this unit's grid
+    uint32_t Eo;       // E - p: E = end of the span's real bytes (bytes >= E are zeroed)
+    uint32_t niters;   // 4 KiB blocks
+    uint32_t aux;      // of the span (initial CRC / stored CRC)
+    uint32_t idx;      // single: span index; else: unit index (slot in seg_raw)
+    uint32_t flags;
+    static constexpr uint32_t kValid = 1, kSingle = 2, kHead = 4, kSane = 8;
+    __device__ __forceinline__ bool valid() const { return flags & kValid; }
+    __device__ __forceinline__ bool single() const { return flags & kSingle; }
+    __device__ __forceinline__ bool head() const { return flags & kHead; }
+    __device__ __forceinline__ bool sane() const { return flags & kSane; }
+    __device__ __forceinline__ const uint8_t *e() const { return p + eo; }
+    __device__ __forceinline__ const uint8_t *E() const { return p + Eo; }
 };
 
 template <int MODE>
 __device__ __forceinline__ UnitDesc fetch_unit(const SpanArgs &a, uint64_t u, uint64_t nunits) {
     UnitDesc d;
-    d.valid = u < nunits;
     d.p = a.base;
-    d.len = 0;
+    d.eo = d.Eo = 0;
     d.aux = 0;
-    d.span_len = 0;
-    d.item = 0;
-    d.unit = u;
-    d.single = true;
-    d.sane = true;
-    if (d.valid) {
+    d.idx = 0;
+    d.flags = 0;
+    d.niters = 0;
+    if (u < nunits) {
         uint32_t seg = kWhole;  // without a unit list every span is one unit
-        d.item = u;
+        uint32_t item = (uint32_t)u;
         if (a.units) {
             const uint2 e = a.units[u];
-            d.item = e.x;
+            item = e.x;
             seg = e.y;
         }
-        const ItemDesc it = fetch_item<MODE>(a, d.item);
+        const ItemDesc it = fetch_item<MODE>(a, item);
+        const uint8_t *E = it.p + it.len;
+        const uint8_t *ea = E + tail_pad(it.p, it.len);
+        const uint32_t nseg = seg == kWhole ? 1u : nseg_of((uint32_t)(ea - it.p));
+        const bool single = nseg == 1, head = single || seg == 0;
+        const uint8_t *e = ea - (size_t)(single ? 0 : nseg - 1 - seg) * kSegBytes;
+        d.p = head ? it.p : e - kSegBytes;
+        d.eo = (uint32_t)(e - d.p);
+        d.Eo = (uint32_t)(E - d.p);
         d.aux = it.aux;
-        d.span_len = it.len;
-        d.sane = it.sane;
-        const uint32_t nseg = seg == kWhole ? 1u : nseg_of(it.len);
-        d.single = nseg == 1;
-        if (d.single) {
-            d.p = it.p;
-            d.len = it.len;
-        } else {
-            const uint8_t *seg_end = it.p + it.len - (size_t)(nseg - 1 - seg) * kSegBytes;
-            d.p = seg == 0 ? it.p : seg_end - kSegBytes;
-            d.len = (uint32_t)(seg_end - d.p);
-        }
+        d.idx = single ? item : (uint32_t)u;
+        d.flags = UnitDesc::kValid | (single ? UnitDesc::kSingle : 0u) | (head ? UnitDesc::kHead : 0u) |
+                  (it.sane ? UnitDesc::kSane : 0u);
+        const uint32_t vlen = d.eo + (uint32_t)((uintptr_t)d.p & 15u);
+        d.niters = it.len ? (vlen + kBlockBytes - 1) / kBlockBytes : 0u;
     }
-    d.npairs = (d.len + kPairBytes - 1) / kPairBytes;
     return d;
 }
 
-template <bool UNALIGNED>
-struct RowWin {
-    static constexpr int NP = UNALIGNED ? 5 : 4;
-    uint4 v[NP];
+struct BlockWin {
+    uint4 v[4][2];  // [row][piece]
 };
 
-template <bool UNALIGNED>
-struct PairWin {
-    RowWin<UNALIGNED> a, b;
-};
-
-// Issue the loads of row pair k of unit d for lane li.
-template <bool UNALIGNED>
-__device__ __forceinline__ void load_pair(PairWin<UNALIGNED> &w, const UnitDesc &d, uint32_t k, uint32_t li,
-                                          const uint4 *zero) {
-    const uint8_t *E = d.p + d.len;
-    const uint8_t *G = E - (size_t)kPairBytes * d.npairs + (size_t)kPairBytes * k;
-    const uint8_t *sa = G + kSpanCH * li;
-    const uint32_t u = UNALIGNED ? (uint32_t)((uintptr_t)E & 15u) : 0u;
-    const uint8_t *wa = sa - u;
-    const uint8_t *wb = wa + kRowBytes;
+// Issue the loads of block k of unit d for lane li.
+__device__ __forceinline__ void load_block(BlockWin &w, const UnitDesc &d, uint32_t k, uint32_t li,
+                                           const uint4 *zero) {
+    const uint8_t *G = d.e() - (size_t)kBlockBytes * (d.niters - k);
+    const uint8_t *E = d.E();
 #pragma unroll
-    for (int j = 0; j < RowWin<UNALIGNED>::NP; ++j) {
-        const uint8_t *pa = wa + 16 * j, *pb = wb + 16 * j;
-        const bool oka = d.valid && pa + 16 > d.p && pa < E;
-        const bool okb = d.valid && pb + 16 > d.p && pb < E;
-        w.a.v[j] = *(oka ? reinterpret_cast<const uint4 *>(pa) : zero);
-        w.b.v[j] = *(okb ? reinterpret_cast<const uint4 *>(pb) : zero);
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint8_t *q = G + r * kRowBytes + kSpanCH * li + 16 * j;
+            const bool ok = q + 16 > d.p && q < E;  // (an invalid unit has E == p)
+            w.v[r][j] = *(ok ? reinterpret_cast<const uint4 *>(q) : zero);
+        }
+}
+
+// Byte masks for dword i of a piece: keep bytes at or after byte k / before byte k.
+__device__ __forceinline__ uint32_t keep_from(uint32_t v, int32_t i, uint32_t k) {
+    int32_t z = (int32_t)k - 4 * i;
+    z = z < 0 ? 0 : z > 4 ? 4 : z;
+    return v & (uint32_t)(0xffffffffull << (8 * z));
+}
+__device__ __forceinline__ uint32_t keep_before(uint32_t v, int32_t i, uint32_t k) {
+    int32_t z = (int32_t)k - 4 * i;
+    z = z < 0 ? 0 : z > 4 ? 4 : z;
+    return v & (uint32_t)((1ull << (8 * z)) - 1ull);
+}
+// Bytes of the 4-byte value x placed at byte offset -d relative to a dword
+// (d = dword position - position of x, in bytes; |d| >= 4 gives 0).
+__device__ __forceinline__ uint32_t place(uint32_t x, int32_t d) {
+    if (d >= 4 || d <= -4) return 0u;
+    return d >= 0 ? x >> (8 * d) : x << (-8 * d);
+}
+
+// Chains over rows NS..3 of a block, folded to the block's lane value.
+template <int NS>
+__device__ __forceinline__ uint32_t block_value(const BlockWin &w, const LaneCtx &c) {
+    uint32_t x[4];
+#pragma unroll
+    for (int r = NS; r < 4; ++r) x[r] = w.v[r][0].x;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int r = NS; r < 4; ++r) {
+            const uint32_t wn = i + 1 < 8 ? dw4(w.v[r][(i + 1) >> 2], (i + 1) & 3) : 0u;
+            x[r] = step4_next(x[r], wn, c);
+        }
     }
-}
-
-// Realign a five-piece window to the 16 chunk dwords starting at byte u.
-__device__ __forceinline__ void realign(const RowWin<true> &w, uint32_t u, uint32_t out[16]) {
-    uint32_t t[20];
+    uint32_t v = x[NS];
 #pragma unroll
-    for (int i = 0; i < 20; ++i) t[i] = dw4(w.v[i >> 2], i & 3);
-    const bool q2 = u & 8u, q1 = u & 4u;
-#pragma unroll
-    for (int i = 0; i < 18; ++i) t[i] = q2 ? t[i + 2] : t[i];
-#pragma unroll
-    for (int i = 0; i < 17; ++i) t[i] = q1 ? t[i + 1] : t[i];
-    const uint32_t b = u & 3u;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) out[i] = __builtin_amdgcn_alignbyte(t[i + 1], t[i], b);
-}
-
-__device__ __forceinline__ void straight(const RowWin<false> &w, uint32_t out[16]) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) out[i] = dw4(w.v[i >> 2], i & 3);
-}
-
-// Zero the chunk bytes that precede the unit start p (lo = p - chunk start).
-__device__ __forceinline__ void mask_head(uint32_t v[16], int64_t lo) {
-    const int32_t l = lo < 0 ? 0 : lo > 64 ? 64 : (int32_t)lo;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        int32_t k = l - 4 * i;
-        k = k < 0 ? 0 : k > 4 ? 4 : k;
-        v[i] &= (uint32_t)(0xffffffffull << (8 * k));
-    }
-}
-
-// Two independent chains (rows A and B) from zero registers, interleaved,
-// with bitop3-fused XORs.
-__device__ __forceinline__ void chain16x2(const uint32_t a[16], const uint32_t b[16], const LaneCtx &c,
-                                          uint32_t &sa, uint32_t &sb) {
-    uint32_t x = a[0], y = b[0];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        x = step4_next(x, i + 1 < 16 ? a[i + 1] : 0u, c);
-        y = step4_next(y, i + 1 < 16 ? b[i + 1] : 0u, c);
-    }
-    sa = x;
-    sb = y;
+    for (int r = NS + 1; r < 4; ++r) v = apply_op<4>(kAuxOp5, v) ^ x[r];
+    return v;
 }
 
 // x^(8*len) mod P from the three-level table (len < 2^30).
@@ -482,16 +481,18 @@ __device__ __forceinline__ uint32_t xpow8_dev(const uint32_t *xp, uint32_t len) 
     return r;
 }
 
-// crc32c(c, D) = ~(M_len(~c) ^ raw(D)), then store (MODE 0) or compare (MODE 1).
+// crc32c(c, D) from raw_v, then store (MODE 0) or compare (MODE 1).
 template <int MODE>
-__device__ __forceinline__ void finalize(const SpanArgs &a, uint64_t item, uint32_t raw, uint32_t aux,
-                                         uint32_t span_len, bool sane) {
-    uint32_t init;
-    if (MODE == 0 && a.lens == nullptr)
-        init = mulmodp_dev(~aux, a.kspan);
-    else
-        init = mulmodp_dev(MODE == 0 ? ~aux : 0xffffffffu, xpow8_dev(a.xpow, span_len));
-    const uint32_t crc = ~(init ^ raw);
+__device__ __forceinline__ void finalize(const SpanArgs &a, uint64_t item, uint32_t raw_v, uint32_t aux,
+                                         const uint8_t *p, uint32_t span_len, bool sane) {
+    const uint32_t t = tail_pad(p, span_len);
+    uint32_t v = raw_v;
+    if (span_len < 4) {  // no room to inject ~crc_in: add M_{len+t}(~crc_in) instead
+        const uint32_t xl = (MODE == 0 && a.lens == nullptr) ? a.kspan16[t] : xpow8_dev(a.xpow, span_len + t);
+        v ^= mulmodp_dev(MODE == 0 ? ~aux : 0xffffffffu, xl);
+    }
+    if (t) v = mulmodp_dev(v, a.xpow[3072 + t]);
+    const uint32_t crc = ~v;
     if (MODE == 0) {
         a.out[item] = crc;
     } else {
@@ -501,7 +502,7 @@ __device__ __forceinline__ void finalize(const SpanArgs &a, uint64_t item, uint3
     }
 }
 
-template <bool UNALIGNED, int MODE>
+template <int MODE>
 __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restrict__ img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     load_tables(smem, img, kLdsImage4Bytes);
@@ -516,50 +517,81 @@ __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restr
 
     UnitDesc cur = fetch_unit<MODE>(a, u, nunits);
     UnitDesc nxt = fetch_unit<MODE>(a, u + ngroups_total, nunits);
-    uint32_t k = 0;    // pair index inside cur
-    uint32_t acc = 0;  // lane accumulator over the pairs of cur
-    PairWin<UNALIGNED> w0, w1;
-    load_pair<UNALIGNED>(w0, cur, 0, li, a.zero);
+    uint32_t k = 0;    // block index inside cur
+    uint32_t acc = 0;  // lane accumulator over the blocks of cur
+    BlockWin w0, w1;
+    load_block(w0, cur, 0, li, a.zero);
 
-    // Process the pair held in `w` (pair k of cur) after issuing the loads of
-    // the group's next pair into `wn`.  Returns false once this group is done.
-    auto step = [&](PairWin<UNALIGNED> &w, PairWin<UNALIGNED> &wn) -> bool {
-        const bool last = k + 1 >= cur.npairs;
+    // Process the block held in `w` (block k of cur) after issuing the loads of
+    // the group's next block into `wn`.  Returns false once this group is done.
+    auto step = [&](BlockWin &w, BlockWin &wn) -> bool {
+        const bool last = k + 1 >= cur.niters;
         if (!last)
-            load_pair<UNALIGNED>(wn, cur, k + 1, li, a.zero);
+            load_block(wn, cur, k + 1, li, a.zero);
         else
-            load_pair<UNALIGNED>(wn, nxt, 0, li, a.zero);
+            load_block(wn, nxt, 0, li, a.zero);
 
-        if (cur.npairs) {
-            uint32_t va[16], vb[16];
-            const uint8_t *E = cur.p + cur.len;
-            const uint8_t *sa = E - (size_t)kPairBytes * cur.npairs + (size_t)kPairBytes * k + kSpanCH * li;
-            if constexpr (UNALIGNED) {
-                const uint32_t uo = (uint32_t)((uintptr_t)E & 15u);
-                realign(w.a, uo, va);
-                realign(w.b, uo, vb);
-            } else {
-                straight(w.a, va);
-                straight(w.b, vb);
+        if (cur.niters) {
+            const uint8_t *G = cur.e() - (size_t)kBlockBytes * (cur.niters - k);
+            const uint8_t *q0 = G + kSpanCH * li;  // this lane's piece 0 of row 0
+            // head: zero the bytes before p and inject ~crc_in into [p, p+4)
+            // (which can spill into the next piece, possibly in block 1)
+            const bool hd = k <= 1 && cur.head();
+            if (__any(hd)) {
+                const uint8_t *ph = (const uint8_t *)((uintptr_t)cur.p & ~(uintptr_t)15);
+                const uint32_t kh = (uint32_t)((uintptr_t)cur.p & 15u);
+                const uint32_t inj = cur.Eo >= 4 ? (MODE == 0 ? ~cur.aux : 0xffffffffu) : 0u;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const uint8_t *q = q0 + r * kRowBytes + 16 * j;
+                        const bool at = hd && q == ph, next = hd && kh > 12 && q == ph + 16;
+                        uint4 &v = w.v[r][j];
+                        const int32_t d = (int32_t)(q - cur.p);  // piece start - p (in [-15, 16] when used)
+                        if (at) {
+                            v.x = keep_from(v.x, 0, kh) ^ place(inj, d);
+                            v.y = keep_from(v.y, 1, kh) ^ place(inj, d + 4);
+                            v.z = keep_from(v.z, 2, kh) ^ place(inj, d + 8);
+                            v.w = keep_from(v.w, 3, kh) ^ place(inj, d + 12);
+                        }
+                        if (next) v.x ^= place(inj, d);
+                    }
             }
-            // Bytes before p inside a loaded piece belong to something else.
-            const int64_t lo = (int64_t)(cur.p - sa);
-            if (__any(lo > 0 && ((uintptr_t)cur.p & 15u))) {
-                mask_head(va, lo);
-                mask_head(vb, lo - (int64_t)kRowBytes);
+            // tail: zero the bytes >= E in the span's last piece
+            const uint32_t te = cur.eo - cur.Eo;
+            const bool ht = last && li == 31 && te - 1u < 15u;
+            if (__any(ht)) {
+                const uint32_t kt = 16u - te;
+                uint4 &v = w.v[3][1];
+                v.x = ht ? keep_before(v.x, 0, kt) : v.x;
+                v.y = ht ? keep_before(v.y, 1, kt) : v.y;
+                v.z = ht ? keep_before(v.z, 2, kt) : v.z;
+                v.w = ht ? keep_before(v.w, 3, kt) : v.w;
             }
-            uint32_t s_a, s_b;
-            chain16x2(va, vb, c, s_a, s_b);
-            acc = xor3(apply_op<4>(kAuxOp6, acc), apply_op<4>(kAuxOp5, s_a), s_b);
+            // rows wholly before p for every lane of the wave are skipped
+            // (a group without a unit has niters == 0 and votes to skip)
+            const uint32_t nskip = __all(G + 3 * kRowBytes <= cur.p)   ? 3u
+                                   : __all(G + 2 * kRowBytes <= cur.p) ? 2u
+                                   : __all(G + kRowBytes <= cur.p)     ? 1u
+                                                                       : 0u;
+            uint32_t v;
+            switch (nskip) {
+                case 0: v = block_value<0>(w, c); break;
+                case 1: v = block_value<1>(w, c); break;
+                case 2: v = block_value<2>(w, c); break;
+                default: v = block_value<3>(w, c); break;
+            }
+            acc = apply_op<4>(kAuxOp6, acc) ^ v;
         }
         if (last) {
-            if (cur.valid) {
+            if (cur.valid()) {
                 const uint32_t raw = group_reduce32_dpp(acc, lane);
                 if (li == 0) {
-                    if (cur.single)
-                        finalize<MODE>(a, cur.item, raw, cur.aux, cur.span_len, cur.sane);
+                    if (cur.single())
+                        finalize<MODE>(a, cur.idx, raw, cur.aux, cur.p, cur.Eo, cur.sane());
                     else
-                        a.seg_raw[cur.unit] = raw;
+                        a.seg_raw[cur.idx] = raw;
                 }
             }
             acc = 0;
@@ -570,7 +602,7 @@ __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restr
         } else {
             ++k;
         }
-        return cur.valid;
+        return cur.valid();
     };
 
     for (;;) {
@@ -584,7 +616,10 @@ template <int MODE>
 __global__ void k_count(SpanArgs a, uint32_t *nseg) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x)
-        nseg[i] = nseg_of(fetch_item<MODE>(a, i).len);
+    {
+        const ItemDesc it = fetch_item<MODE>(a, i);
+        nseg[i] = nseg_of(it.len + tail_pad(it.p, it.len));
+    }
 }
 
 // Write unit descriptors at prefix[i].  Spans whose units would pass `cap`
@@ -618,7 +653,7 @@ __global__ void k_combine(SpanArgs a, const uint32_t *nseg, const uint32_t *pref
         uint32_t acc = 0;
         for (uint32_t s = 0; s < ns; ++s) acc = mulmodp_dev(acc, kseg) ^ a.seg_raw[p0 + s];
         const ItemDesc it = fetch_item<MODE>(a, i);
-        finalize<MODE>(a, i, acc, it.aux, it.len, it.sane);
+        finalize<MODE>(a, i, acc, it.aux, it.p, it.len, it.sane);
     }
 }
 

@@ -53,6 +53,7 @@ constexpr int kBlock = 1024;                    // 16 waves, 32 lane groups
 constexpr uint32_t kItemsPerBlockStep = 32;     // one span per 32-lane group
 constexpr uint32_t kFixedLen = 4096;            // K1 instance: 4 rows x 32 lanes x 32 B
 constexpr uint32_t kFixedCH = 32;
+static_assert(kFixedCH == mcrc_dev::kSpanCH, "K1 and the span kernels share one table image");
 #define K1_KERNEL mcrc_dev::k_fixed<4, 32, kFixedCH, 4, 5>
 
 thread_local float g_last_kernel_ms = -1.0f;
@@ -61,8 +62,8 @@ struct Device {
     int id = -1;
     int cus = 0;
     bool ok = false;
-    uint4 *img = nullptr;       // LDS table image for the span kernels (CH = 64)
-    uint4 *img_k1 = nullptr;    // LDS table image for K1 (CH = 32)
+    uint4 *img = nullptr;       // LDS table image (CH = 32) for every kernel
+    uint4 *img_k1 = nullptr;    // alias of img
     uint32_t *xpow = nullptr;   // 3 x 1024 x^(8n) table
     uint4 *zero = nullptr;      // 16 zero bytes
     unsigned long long *nbad = nullptr;
@@ -115,17 +116,16 @@ int init_device(Device &d, int id) {
     d.cus = p.multiProcessorCount;
     std::vector<uint32_t> img(mcrc::kImage4Dwords);
     mcrc::build_lds_image4(img.data(), mcrc_dev::kSpanCH);
-    std::vector<uint32_t> xp(3 * 1024);
+    std::vector<uint32_t> xp(3 * 1024 + 16);
     for (uint32_t j = 0; j < 1024; ++j) {
         xp[j] = mcrc::xpow8n(j);
         xp[1024 + j] = mcrc::xpow8n((uint64_t)j << 10);
         xp[2048 + j] = mcrc::xpow8n((uint64_t)j << 20);
     }
+    for (uint32_t t = 0; t < 16; ++t) xp[3072 + t] = mcrc::xpow8n_inv(t);
     HIP_OK(hipMalloc(&d.img, img.size() * 4));
     HIP_OK(hipMemcpy(d.img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
-    mcrc::build_lds_image4(img.data(), kFixedCH);
-    HIP_OK(hipMalloc(&d.img_k1, img.size() * 4));
-    HIP_OK(hipMemcpy(d.img_k1, img.data(), img.size() * 4, hipMemcpyHostToDevice));
+    d.img_k1 = d.img;  // K1 and the span kernels share the CH = 32 image
     HIP_OK(hipMalloc(&d.xpow, xp.size() * 4));
     HIP_OK(hipMemcpy(d.xpow, xp.data(), xp.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&d.zero, 64));
@@ -136,8 +136,7 @@ int init_device(Device &d, int id) {
     HIP_OK(hipEventCreate(&d.ev0));
     HIP_OK(hipEventCreate(&d.ev1));
     const void *kernels[] = {
-        (const void *)K1_KERNEL,                            (const void *)mcrc_dev::k_spans<false, 0>,
-        (const void *)mcrc_dev::k_spans<true, 0>,           (const void *)mcrc_dev::k_spans<true, 1>,
+        (const void *)K1_KERNEL, (const void *)mcrc_dev::k_spans<0>, (const void *)mcrc_dev::k_spans<1>,
     };
     for (const void *k : kernels)
         HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImage4Bytes));
@@ -206,13 +205,10 @@ template <int MODE>
 int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) {
     const uint64_t n = a.n;
     const bool identity = MODE == 0 && a.lens == nullptr && a.len <= mcrc_dev::kSegBytes;
+    (void)aligned;
     auto spans = [&](const mcrc_dev::SpanArgs &x, int grid) {
-        if (aligned && MODE == 0)
-            hipLaunchKernelGGL((mcrc_dev::k_spans<false, MODE>), dim3(grid), dim3(kBlock),
-                               mcrc_dev::kLdsImage4Bytes, st, x, d.img);
-        else
-            hipLaunchKernelGGL((mcrc_dev::k_spans<true, MODE>), dim3(grid), dim3(kBlock),
-                               mcrc_dev::kLdsImage4Bytes, st, x, d.img);
+        hipLaunchKernelGGL((mcrc_dev::k_spans<MODE>), dim3(grid), dim3(kBlock), mcrc_dev::kLdsImage4Bytes, st,
+                           x, d.img);
     };
     if (identity) {
         spans(a, grid_for(d, n));
@@ -221,7 +217,7 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     if (n >= 0xffffffffull) return CRC32C_EINVAL;
     // units fit in cap whenever the spans do not overlap; overlapping long spans
     // past cap are processed whole by the second span pass
-    const uint64_t cap = std::min<uint64_t>(n + a.base_bytes / mcrc_dev::kSegBytes + 1, 0xfffffff0ull);
+    const uint64_t cap = std::min<uint64_t>(n + a.base_bytes / mcrc_dev::kSegBytes + 1 + n / 4096, 0xfffffff0ull);
     int rc = ensure_plan(d, n, cap);
     if (rc) return rc;
     uint32_t *nvalid = d.counters, *nwhole = d.counters + 1;
@@ -266,7 +262,8 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
     a.stride = s.stride;
     a.lens = s.lens;
     a.len = s.len;
-    a.kspan = kspan;
+    if (s.lens == nullptr)
+        for (uint32_t t = 0; t < 16; ++t) a.kspan16[t] = mcrc::xpow8n((uint64_t)s.len + t);
     a.crc_in = s.crc_in;
     a.out = s.out;
     a.n = s.n;
