@@ -184,12 +184,12 @@ def workload_config3(args, rank, world):
 
 def run_verify_steps(args_v, steps: int, stream):
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    base, size, offs, n, ok = args_v
+    base, size, region, offs, n, ok = args_v
     nbad = ctypes.c_uint64(0)
     for a, b in evs:
         a.record(stream)
-        _lib.check(_lib.lib.crc32c_verify_items(base, size, offs, n, ok, ctypes.byref(nbad), _lib.CRC32C_DEVICE,
-                                                ctypes.c_void_p(stream.cuda_stream)))
+        _lib.check(_lib.lib.crc32c_verify_items(base, size, region, offs, n, ok, ctypes.byref(nbad),
+                                                _lib.CRC32C_DEVICE, ctypes.c_void_p(stream.cuda_stream)))
         b.record(stream)
     return evs, int(nbad.value)
 
@@ -243,7 +243,7 @@ def workload_config5(args, rank, world):
     flat[pos] ^= (torch.ones_like(bit) << bit)
     ok = torch.empty(n, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
-    return (data.data_ptr(), data.numel(), offs.data_ptr(), n, ok.data_ptr()), ok, victims, \
+    return (data.data_ptr(), data.numel(), wbuf, offs.data_ptr(), n, ok.data_ptr()), ok, victims, \
         n * (ntotal - 32), {
             "workload": f"BASELINE configs[4]: {args.pages} x 64 MiB extstore pages, 16 wbufs x 1007 packed "
                         "4165-B item images each, stored CRC verified per item (K3 k_spans<verify>)",

@@ -76,9 +76,13 @@ int crc32c_batch_multi(const crc32c_spans *spans, int ngpus);
 
 /* Verify n item images of a packed page buffer (host or device per flags).
  * ok[i] = 1 when item i's CRC matches its stored exptime; *nbad receives the
- * number of mismatching (or malformed) items. */
-int crc32c_verify_items(const void *base, uint64_t base_bytes, const uint64_t *item_offsets,
-                        uint64_t n, uint8_t *ok, uint64_t *nbad, unsigned flags, void *stream);
+ * number of mismatching (or malformed) items.  region_bytes is the write
+ * buffer size: extstore never lets an item cross a wbuf (extstore.c:627-636),
+ * so an image whose header claims to is malformed (0 = bound by base_bytes
+ * only). */
+int crc32c_verify_items(const void *base, uint64_t base_bytes, uint64_t region_bytes,
+                        const uint64_t *item_offsets, uint64_t n, uint8_t *ok, uint64_t *nbad,
+                        unsigned flags, void *stream);
 
 /* Asynchronous form of crc32c_batch for host batches: returns at once with a
  * job handle; crc32c_batch_wait blocks until out[] is filled and frees it. */

@@ -11,7 +11,8 @@ import ctypes
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libmcrc32c.so")
+# MCRC_LIB selects another build of the same library (ablation builds, tools/ablate_spans.sh)
+LIB_PATH = os.environ.get("MCRC_LIB") or os.path.join(PKG, "libmcrc32c.so")
 
 CRC32C_OK = 0
 CRC32C_ENODEV = -1
@@ -69,7 +70,8 @@ def _load():
     lib.crc32c_batch_multi.restype = ctypes.c_int
     lib.crc32c_batch_multi.argtypes = [ctypes.POINTER(Spans), ctypes.c_int]
     lib.crc32c_verify_items.restype = ctypes.c_int
-    lib.crc32c_verify_items.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+    lib.crc32c_verify_items.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                        ctypes.c_uint64,
                                         ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint,
                                         ctypes.c_void_p]
     lib.crc32c_batch_submit.restype = ctypes.c_int

@@ -116,8 +116,12 @@ def batch_multi(buf, offsets=None, stride: int = 0, lens=None, length: int = 0, 
     return out
 
 
-def verify_items(buf, item_offsets, stream=None):
-    """Verify packed item images; returns (ok uint8 array / tensor, nbad)."""
+def verify_items(buf, item_offsets, region_bytes=0, stream=None):
+    """Verify packed item images; returns (ok uint8 array / tensor, nbad).
+
+    ``region_bytes``: the write-buffer size; an item whose header claims a
+    span crossing a multiple of it is reported bad without being read
+    (extstore never splits an item across wbufs).  0 = no such bound."""
     dev = _is_torch(buf) and buf.is_cuda
     nbad = ctypes.c_uint64(0)
     if dev:
@@ -126,13 +130,14 @@ def verify_items(buf, item_offsets, stream=None):
         ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
         if stream is None:
             stream = torch.cuda.current_stream(buf.device).cuda_stream
-        rc = lib.crc32c_verify_items(buf.data_ptr(), buf.numel() * buf.element_size(), item_offsets.data_ptr(),
-                                     n, ok.data_ptr(), ctypes.byref(nbad), CRC32C_DEVICE, stream)
+        rc = lib.crc32c_verify_items(buf.data_ptr(), buf.numel() * buf.element_size(), region_bytes,
+                                     item_offsets.data_ptr(), n, ok.data_ptr(), ctypes.byref(nbad), CRC32C_DEVICE,
+                                     stream)
     else:
         buf = _host_buf(buf)
         offs = np.ascontiguousarray(item_offsets, dtype=np.uint64)
         ok = np.empty(offs.size, dtype=np.uint8)
-        rc = lib.crc32c_verify_items(buf.ctypes.data, buf.size, offs.ctypes.data, offs.size, ok.ctypes.data,
-                                     ctypes.byref(nbad), 0, None)
+        rc = lib.crc32c_verify_items(buf.ctypes.data, buf.size, region_bytes, offs.ctypes.data, offs.size,
+                                     ok.ctypes.data, ctypes.byref(nbad), 0, None)
     check(rc, "crc32c_verify_items")
     return ok, int(nbad.value)

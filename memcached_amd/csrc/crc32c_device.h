@@ -39,6 +39,10 @@ constexpr uint32_t kAuxOp6 = 24;  // M_{128*CH}
 constexpr uint32_t kLdsImage1Bytes = 256 * 64 * 4;              // 64 KiB
 constexpr uint32_t kAux4Bytes = 28 * 1024;                        // 28 KiB
 constexpr uint32_t kLdsImage4Bytes = kAux4Bytes + 2 * 65536;     // 156 KiB
+// Span kernels append 16 rows of 32 dwords: row t, dword i = x^(i - 8t) mod P
+// (the lane-distributed multiply by x^(-8t), crc32c_kernels.hip mul_xinv_group).
+constexpr uint32_t kXinvOffset = kLdsImage4Bytes;
+constexpr uint32_t kLdsSpanBytes = kLdsImage4Bytes + 16 * 32 * 4;  // 158 KiB
 constexpr uint32_t kPoly = 0x82f63b78u;
 
 template <int SLICE>

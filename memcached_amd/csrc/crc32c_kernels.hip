@@ -310,9 +310,11 @@ struct SpanArgs {
     const uint32_t *xpow;      // x^(8*j), x^(8*1024*j), x^(8*2^20*j) (3 x 1024), x^(-8t) (16)
     const uint4 *zero;         // 16 zero bytes in device memory
     // work units (nullptr: unit u = span u, one segment)
-    const uint2 *units;        // (span index, segment index or kWhole)
+    const struct UnitRec *units;
     const uint32_t *nunits;    // device-side unit count
-    uint32_t *seg_raw;         // raw_v of each unit of a multi-segment span
+    uint32_t *span_acc;        // multi-segment spans: XOR of the shifted segment values
+    const uint32_t *segpow;    // rows k (x^i * x^(8 * 64Ki * k), i < 32) for k < 256, then k = 256 j
+    uint64_t region;           // MODE 1: items never cross a multiple of `region` (0: no bound)
 };
 
 struct ItemDesc {
@@ -355,22 +357,34 @@ __device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
         const uint32_t nkey = hdr_ok ? ld_u8(it + 41) : 0u;
         const uint64_t ntotal = 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) + ((flags & 2u) ? 8 : 0);
         d.aux = hdr_ok ? ld_u32_unaligned(it + 28) : 0u;
-        d.sane = hdr_ok && nkey != 0 && nbytes < 0x80000000u && off + ntotal <= a.base_bytes;
+        // an item never crosses its write buffer (extstore.c:627-636), so a
+        // header claiming otherwise is corrupt
+        const bool in_region = a.region == 0 || off / a.region == (off + ntotal - 1) / a.region;
+        d.sane = hdr_ok && nkey != 0 && nbytes < 0x80000000u && off + ntotal <= a.base_bytes && in_region;
         d.p = it + 32;
         d.len = d.sane ? (uint32_t)(ntotal - 32) : 0u;
     }
     return d;
 }
 
-// Descriptor of one work unit, kept compact (two are live per lane).
+// Work-unit record written by k_expand (32 B, one dwordx4 pair per unit):
+//   a = {offset of the unit's first byte from base (lo, hi), e - p, E - p}
+//   b = {aux, span index, flags | niters << 8, nseg - 1 - segment}
+struct alignas(16) UnitRec {
+    uint4 a, b;
+};
+
+// Item record written by k_count: {offset of the span (lo, hi | !sane << 31), len, aux}.
+constexpr uint32_t kInsane = 0x80000000u;
+
+// Decoded descriptor of one work unit (two are live per lane).
 struct UnitDesc {
     const uint8_t *p;  // first byte of this unit
     uint32_t eo;       // e - p: e = 16-aligned end of this unit's grid
     uint32_t Eo;       // E - p: E = end of the span's real bytes (bytes >= E are zeroed)
     uint32_t niters;   // 4 KiB blocks
-    uint32_t aux;      // of the span (initial CRC / stored CRC)
-    uint32_t idx;      // single: span index; else: unit index (slot in seg_raw)
     uint32_t flags;
+    uint32_t raw;      // this lane's dword of the raw record (aux = dword 4, span index = dword 5)
     static constexpr uint32_t kValid = 1, kSingle = 2, kHead = 4, kSane = 8;
     __device__ __forceinline__ bool valid() const { return flags & kValid; }
     __device__ __forceinline__ bool single() const { return flags & kSingle; }
@@ -380,39 +394,68 @@ struct UnitDesc {
     __device__ __forceinline__ const uint8_t *E() const { return p + Eo; }
 };
 
-template <int MODE>
-__device__ __forceinline__ UnitDesc fetch_unit(const SpanArgs &a, uint64_t u, uint64_t nunits) {
-    UnitDesc d;
-    d.p = a.base;
-    d.eo = d.Eo = 0;
-    d.aux = 0;
-    d.idx = 0;
-    d.flags = 0;
-    d.niters = 0;
-    if (u < nunits) {
-        uint32_t seg = kWhole;  // without a unit list every span is one unit
-        uint32_t item = (uint32_t)u;
-        if (a.units) {
-            const uint2 e = a.units[u];
-            item = e.x;
-            seg = e.y;
+// Unit (segment `seg` of span [base + off, +len), or the whole span) as a record.
+__device__ __forceinline__ UnitRec make_unit(const uint8_t *base, uint64_t off, uint32_t len, uint32_t aux,
+                                             bool sane, uint32_t item, uint32_t seg) {
+    const uint8_t *p0 = base + off;
+    const uint32_t vlen = len + tail_pad(p0, len);
+    const uint32_t nseg = seg == kWhole ? 1u : nseg_of(vlen);
+    const bool single = nseg == 1, head = single || seg == 0;
+    const uint32_t eo0 = vlen - (single ? 0u : (nseg - 1 - seg) * kSegBytes);  // e - p0
+    const uint32_t po = head ? 0u : eo0 - kSegBytes;                          // p - p0
+    const uint32_t eo = eo0 - po;
+    const uint32_t niters = len ? (eo + (uint32_t)((uintptr_t)(p0 + po) & 15u) + kBlockBytes - 1) / kBlockBytes : 0u;
+    const uint64_t o = off + po;
+    UnitRec r;
+    r.a = make_uint4((uint32_t)o, (uint32_t)(o >> 32), eo, len - po);
+    r.b = make_uint4(aux, item,
+                     UnitDesc::kValid | (single ? UnitDesc::kSingle : 0u) | (head ? UnitDesc::kHead : 0u) |
+                         (sane ? UnitDesc::kSane : 0u) | (niters << 8),
+                     single ? 0u : nseg - 1 - seg);
+    return r;
+}
+
+// Raw fetch of unit u.  The record is the same for every lane of a group, so
+// lane j of the group holds only its dword j (one VGPR while the loads are in
+// flight); decode_unit gathers the dwords when the unit is first needed, so the
+// group keeps streaming meanwhile.
+template <int MODE, bool UNITS>
+__device__ __forceinline__ uint32_t fetch_unit(const SpanArgs &a, uint64_t u, uint64_t nunits, uint32_t li) {
+    const uint32_t j = li & 7u;
+    if (u >= nunits) return 0u;  // flags 0: no unit
+    if (UNITS) return reinterpret_cast<const uint32_t *>(a.units + u)[j];
+    // MODE 0, one unit per span: raw item fields {off lo, off hi, len, -, crc_in, u, 1, -}
+    switch (j) {
+        case 0:
+        case 1: {
+            const uint64_t off = a.offsets ? a.offsets[u] : u * a.stride;
+            return (uint32_t)(off >> (32 * j));
         }
-        const ItemDesc it = fetch_item<MODE>(a, item);
-        const uint8_t *E = it.p + it.len;
-        const uint8_t *ea = E + tail_pad(it.p, it.len);
-        const uint32_t nseg = seg == kWhole ? 1u : nseg_of((uint32_t)(ea - it.p));
-        const bool single = nseg == 1, head = single || seg == 0;
-        const uint8_t *e = ea - (size_t)(single ? 0 : nseg - 1 - seg) * kSegBytes;
-        d.p = head ? it.p : e - kSegBytes;
-        d.eo = (uint32_t)(e - d.p);
-        d.Eo = (uint32_t)(E - d.p);
-        d.aux = it.aux;
-        d.idx = single ? item : (uint32_t)u;
-        d.flags = UnitDesc::kValid | (single ? UnitDesc::kSingle : 0u) | (head ? UnitDesc::kHead : 0u) |
-                  (it.sane ? UnitDesc::kSane : 0u);
-        const uint32_t vlen = d.eo + (uint32_t)((uintptr_t)d.p & 15u);
-        d.niters = it.len ? (vlen + kBlockBytes - 1) / kBlockBytes : 0u;
+        case 2: return a.lens ? a.lens[u] : a.len;
+        case 4: return a.crc_in ? a.crc_in[u] : 0u;
+        case 5: return (uint32_t)u;
+        case 6: return 1u;
+        default: return 0u;
     }
+}
+
+template <int MODE, bool UNITS>
+__device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw, uint32_t lane) {
+    const uint32_t g = lane & 32u;
+    UnitRec r;
+    r.a = make_uint4(__shfl(raw, g | 0, 64), __shfl(raw, g | 1, 64), __shfl(raw, g | 2, 64), __shfl(raw, g | 3, 64));
+    r.b = make_uint4(__shfl(raw, g | 4, 64), __shfl(raw, g | 5, 64), __shfl(raw, g | 6, 64), 0u);
+    if (!UNITS && r.b.z) {
+        const uint64_t off = r.a.x | ((uint64_t)r.a.y << 32);
+        r = make_unit(a.base, off, r.a.z, r.b.x, true, r.b.y, kWhole);
+    }
+    UnitDesc d;  // (aux and the span index stay in raw: read at the unit's end)
+    d.p = a.base + (r.a.x | ((uint64_t)r.a.y << 32));
+    d.eo = r.a.z;
+    d.Eo = r.a.w;
+    d.raw = raw;
+    d.flags = r.b.z & 0xffu;
+    d.niters = r.b.z >> 8;
     return d;
 }
 
@@ -481,18 +524,9 @@ __device__ __forceinline__ uint32_t xpow8_dev(const uint32_t *xp, uint32_t len) 
     return r;
 }
 
-// crc32c(c, D) from raw_v, then store (MODE 0) or compare (MODE 1).
+// Store (MODE 0) or compare (MODE 1) the final CRC of span `item`.
 template <int MODE>
-__device__ __forceinline__ void finalize(const SpanArgs &a, uint64_t item, uint32_t raw_v, uint32_t aux,
-                                         const uint8_t *p, uint32_t span_len, bool sane) {
-    const uint32_t t = tail_pad(p, span_len);
-    uint32_t v = raw_v;
-    if (span_len < 4) {  // no room to inject ~crc_in: add M_{len+t}(~crc_in) instead
-        const uint32_t xl = (MODE == 0 && a.lens == nullptr) ? a.kspan16[t] : xpow8_dev(a.xpow, span_len + t);
-        v ^= mulmodp_dev(MODE == 0 ? ~aux : 0xffffffffu, xl);
-    }
-    if (t) v = mulmodp_dev(v, a.xpow[3072 + t]);
-    const uint32_t crc = ~v;
+__device__ __forceinline__ void emit(const SpanArgs &a, uint64_t item, uint32_t crc, uint32_t aux, bool sane) {
     if (MODE == 0) {
         a.out[item] = crc;
     } else {
@@ -502,21 +536,75 @@ __device__ __forceinline__ void finalize(const SpanArgs &a, uint64_t item, uint3
     }
 }
 
+// M_{len+t}(~crc_in) for a span too short (< 4 B) to carry the injected ~crc_in.
 template <int MODE>
-__global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restrict__ img) {
+__device__ __forceinline__ uint32_t short_init(const SpanArgs &a, uint32_t aux, uint32_t len, uint32_t t) {
+    const uint32_t xl = (MODE == 0 && a.lens == nullptr) ? a.kspan16[t] : xpow8_dev(a.xpow, len + t);
+    return mulmodp_dev(MODE == 0 ? ~aux : 0xffffffffu, xl);
+}
+
+// crc32c(c, D) from raw_v (one thread; k_combine).
+template <int MODE>
+__device__ __forceinline__ void finalize(const SpanArgs &a, uint64_t item, uint32_t raw_v, uint32_t aux,
+                                         const uint8_t *p, uint32_t span_len, bool sane) {
+    const uint32_t t = tail_pad(p, span_len);
+    uint32_t v = raw_v;
+    if (span_len < 4) v ^= short_init<MODE>(a, aux, span_len, t);
+    if (t) v = mulmodp_dev(v, a.xpow[3072 + t]);
+    emit<MODE>(a, item, ~v, aux, sane);
+}
+
+// v0 (lane 0 of the group) times the element whose row `row` holds
+// x^i * element (i < 32) in global memory; the product lands in lane 0.
+__device__ __forceinline__ uint32_t mul_row_group(uint32_t v0, const uint32_t *row, uint32_t li) {
+    const uint32_t v = __shfl(v0, 0, 32);
+    uint32_t term = (v << li) & 0x80000000u ? row[li] : 0u;
+    term ^= lane_down<0>(term);
+    term ^= lane_down<1>(term);
+    term ^= lane_down<2>(term);
+    term ^= lane_down<3>(term);
+    term ^= lane_down<4>(term);
+    return term;
+}
+
+// v * x^(-8t) mod P spread over a 32-lane group: lane i adds bit i of v (the
+// x^i coefficient) times x^(i-8t) from the LDS table, and the lanes XOR-reduce
+// into lane 0.  v is read from lane 0 of the group; t is per group.
+__device__ __forceinline__ uint32_t mul_xinv_group(uint32_t v0, uint32_t t, uint32_t li) {
+    const uint32_t v = __shfl(v0, 0, 32);
+    uint32_t term = (v << li) & 0x80000000u ? lds_ld(kXinvOffset + (t << 7) + (li << 2)) : 0u;
+    term ^= lane_down<0>(term);
+    term ^= lane_down<1>(term);
+    term ^= lane_down<2>(term);
+    term ^= lane_down<3>(term);
+    term ^= lane_down<4>(term);
+    return term;
+}
+
+#ifndef MCRC_SPAN_BLOCK
+#define MCRC_SPAN_BLOCK 1024
+#endif
+// 16 waves per CU (128 VGPRs).  768 threads (168 VGPRs) removes the few
+// remaining spills but measured slower (config 3: 5.99 vs 5.90 ms; config 5:
+// 6.90 vs 5.93 ms per 300 pages): latency hiding of the dependent lookup
+// chains needs the waves more than the spilled registers cost.
+constexpr uint32_t kSpanBlock = MCRC_SPAN_BLOCK;
+
+template <int MODE, bool UNITS>
+__global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *__restrict__ img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    load_tables(smem, img, kLdsImage4Bytes);
+    load_tables(smem, img, kLdsSpanBytes);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t li = lane & 31u;
     LaneCtx c;
     c.lane4 = li << 2;
     c.lane4hi = c.lane4 | 0x10000u;
-    const uint64_t nunits = a.units ? (uint64_t)*a.nunits : a.n;
+    const uint64_t nunits = UNITS ? (uint64_t)*a.nunits : a.n;
     const uint64_t ngroups_total = (uint64_t)gridDim.x * (blockDim.x >> 5);
     uint64_t u = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
 
-    UnitDesc cur = fetch_unit<MODE>(a, u, nunits);
-    UnitDesc nxt = fetch_unit<MODE>(a, u + ngroups_total, nunits);
+    UnitDesc cur = decode_unit<MODE, UNITS>(a, fetch_unit<MODE, UNITS>(a, u, nunits, li), lane);
+    uint32_t nxt = fetch_unit<MODE, UNITS>(a, u + ngroups_total, nunits, li);  // decoded when first needed
     uint32_t k = 0;    // block index inside cur
     uint32_t acc = 0;  // lane accumulator over the blocks of cur
     BlockWin w0, w1;
@@ -526,21 +614,28 @@ __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restr
     // the group's next block into `wn`.  Returns false once this group is done.
     auto step = [&](BlockWin &w, BlockWin &wn) -> bool {
         const bool last = k + 1 >= cur.niters;
-        if (!last)
+        UnitDesc nd;
+        if (!last) {
             load_block(wn, cur, k + 1, li, a.zero);
-        else
-            load_block(wn, nxt, 0, li, a.zero);
+        } else {
+            nd = decode_unit<MODE, UNITS>(a, nxt, lane);
+            load_block(wn, nd, 0, li, a.zero);
+        }
 
         if (cur.niters) {
             const uint8_t *G = cur.e() - (size_t)kBlockBytes * (cur.niters - k);
             const uint8_t *q0 = G + kSpanCH * li;  // this lane's piece 0 of row 0
             // head: zero the bytes before p and inject ~crc_in into [p, p+4)
             // (which can spill into the next piece, possibly in block 1)
+#ifdef MCRC_ABL_NOHEAD  // ablation: skip head masking and ~crc_in injection (wrong CRCs)
+            const bool hd = false;
+#else
             const bool hd = k <= 1 && cur.head();
+#endif
             if (__any(hd)) {
                 const uint8_t *ph = (const uint8_t *)((uintptr_t)cur.p & ~(uintptr_t)15);
                 const uint32_t kh = (uint32_t)((uintptr_t)cur.p & 15u);
-                const uint32_t inj = cur.Eo >= 4 ? (MODE == 0 ? ~cur.aux : 0xffffffffu) : 0u;
+                const uint32_t inj = cur.Eo < 4 ? 0u : MODE == 0 ? ~__shfl(cur.raw, (lane & 32u) | 4u, 64) : 0xffffffffu;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -586,19 +681,28 @@ __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restr
         }
         if (last) {
             if (cur.valid()) {
-                const uint32_t raw = group_reduce32_dpp(acc, lane);
-                if (li == 0) {
-                    if (cur.single())
-                        finalize<MODE>(a, cur.idx, raw, cur.aux, cur.p, cur.Eo, cur.sane());
-                    else
-                        a.seg_raw[cur.idx] = raw;
+                uint32_t raw = group_reduce32_dpp(acc, lane);
+                if (cur.single()) {
+                    const uint32_t t = cur.eo - cur.Eo;  // tail padding
+                    const uint32_t aux = __shfl(cur.raw, (lane & 32u) | 4u, 64);
+                    const uint32_t item = __shfl(cur.raw, (lane & 32u) | 5u, 64);
+                    if (li == 0 && cur.Eo < 4) raw ^= short_init<MODE>(a, aux, cur.Eo, t);
+                    const uint32_t v = mul_xinv_group(raw, t, li);
+                    if (li == 0) emit<MODE>(a, item, ~v, aux, cur.sane());
+                } else {
+                    // segment s of nseg: raw_v(span) gets M_{64Ki * (nseg-1-s)}(raw)
+                    const uint32_t k = __shfl(cur.raw, (lane & 32u) | 7u, 64);
+                    const uint32_t item = __shfl(cur.raw, (lane & 32u) | 5u, 64);
+                    uint32_t v = mul_row_group(raw, a.segpow + 32 * (k & 255u), li);
+                    v = mul_row_group(v, a.segpow + 32 * (256 + (k >> 8)), li);
+                    if (li == 0) atomicXor(a.span_acc + item, v);
                 }
             }
             acc = 0;
             k = 0;
             u += ngroups_total;
-            cur = nxt;
-            nxt = fetch_unit<MODE>(a, u + ngroups_total, nunits);
+            cur = nd;
+            nxt = fetch_unit<MODE, UNITS>(a, u + ngroups_total, nunits, li);
         } else {
             ++k;
         }
@@ -611,49 +715,56 @@ __global__ __launch_bounds__(1024) void k_spans(SpanArgs a, const uint4 *__restr
     }
 }
 
-// Segments per span (for the exclusive scan that places the work units).
+// Segments per span (for the exclusive scan that places the work units), and
+// the span's item record (the header is parsed once per launch).
 template <int MODE>
-__global__ void k_count(SpanArgs a, uint32_t *nseg) {
+__global__ void k_count(SpanArgs a, uint32_t *nseg, uint4 *irec) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x)
     {
         const ItemDesc it = fetch_item<MODE>(a, i);
         nseg[i] = nseg_of(it.len + tail_pad(it.p, it.len));
+        const uint64_t off = (uint64_t)(it.p - a.base);
+        irec[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32) | (it.sane ? 0u : kInsane), it.len, it.aux);
+        a.span_acc[i] = 0u;
     }
 }
 
-// Write unit descriptors at prefix[i].  Spans whose units would pass `cap`
-// (possible only when spans overlap) are listed in `whole` and processed as
-// one unit each by a second pass; *nvalid = units written before the first
+// Write the unit records of span i at prefix[i].  Spans whose units would pass
+// `cap` (possible only when spans overlap) are listed in `whole` and processed
+// as one unit each by a second pass; *nvalid = units written before the first
 // such span.
-__global__ void k_expand(const uint32_t *nseg, const uint32_t *prefix, uint64_t n, uint2 *units, uint64_t cap,
-                         uint32_t *nvalid, uint2 *whole, uint32_t *nwhole) {
+__global__ void k_expand(const uint8_t *base, const uint32_t *nseg, const uint32_t *prefix, const uint4 *irec,
+                         uint64_t n, UnitRec *units, uint64_t cap, uint32_t *nvalid, UnitRec *whole,
+                         uint32_t *nwhole) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t p0 = prefix[i], ns = nseg[i];
+        const uint4 r = irec[i];
+        const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
+        const bool sane = !(r.y & kInsane);
         if (p0 + ns <= cap) {
-            for (uint32_t s = 0; s < ns; ++s) units[p0 + s] = make_uint2((uint32_t)i, s);
+            for (uint32_t s = 0; s < ns; ++s) units[p0 + s] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, s);
             if (i + 1 == n) *nvalid = (uint32_t)(p0 + ns);
         } else {
             if (p0 <= cap) atomicMin(nvalid, (uint32_t)p0);
-            whole[atomicAdd(nwhole, 1u)] = make_uint2((uint32_t)i, kWhole);
+            whole[atomicAdd(nwhole, 1u)] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, kWhole);
         }
     }
 }
 
-// Fold the segment CRCs of every multi-segment span (one thread per span).
+// Finalise every multi-segment span from its accumulated raw value (one
+// thread per span; the segment units already shifted and XORed their values).
 template <int MODE>
-__global__ void k_combine(SpanArgs a, const uint32_t *nseg, const uint32_t *prefix, const uint32_t *nvalid,
-                          uint32_t kseg) {
+__global__ void k_combine(SpanArgs a, const uint32_t *nseg, const uint32_t *prefix, const uint4 *irec,
+                          const uint32_t *nvalid) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t ns = nseg[i];
-        const uint64_t p0 = prefix[i];
-        if (ns <= 1 || p0 + ns > *nvalid) continue;  // single, or processed whole
-        uint32_t acc = 0;
-        for (uint32_t s = 0; s < ns; ++s) acc = mulmodp_dev(acc, kseg) ^ a.seg_raw[p0 + s];
-        const ItemDesc it = fetch_item<MODE>(a, i);
-        finalize<MODE>(a, i, acc, it.aux, it.p, it.len, it.sane);
+        if (ns <= 1 || prefix[i] + (uint64_t)ns > *nvalid) continue;  // single, or processed whole
+        const uint4 r = irec[i];
+        const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
+        finalize<MODE>(a, i, a.span_acc[i], r.w, a.base + off, r.z, !(r.y & kInsane));
     }
 }
 

@@ -80,8 +80,10 @@ struct Device {
     uint32_t *hlens[2] = {nullptr, nullptr}, *hcin[2] = {nullptr, nullptr}, *hout[2] = {nullptr, nullptr};
     uint64_t slot_items = 0;
     // work-unit planning for long / variable spans (grow-only)
-    uint32_t *nseg = nullptr, *prefix = nullptr, *seg_raw = nullptr, *counters = nullptr;
-    uint2 *units = nullptr, *whole = nullptr;
+    uint32_t *nseg = nullptr, *prefix = nullptr, *span_acc = nullptr, *counters = nullptr;
+    uint32_t *segpow = nullptr;  // rows x^i * x^(8*64Ki*k): k < 256, then k = 256 j
+    mcrc_dev::UnitRec *units = nullptr, *whole = nullptr;
+    uint4 *irec = nullptr;  // per-span record written by k_count
     void *scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
     uint64_t plan_items = 0, plan_units = 0;
@@ -114,8 +116,13 @@ int init_device(Device &d, int id) {
     HIP_OK(hipGetDeviceProperties(&p, id));
     if (strncmp(p.gcnArchName, "gfx950", 6) != 0) return CRC32C_ENODEV;
     d.cus = p.multiProcessorCount;
-    std::vector<uint32_t> img(mcrc::kImage4Dwords);
+    std::vector<uint32_t> img(mcrc_dev::kLdsSpanBytes / 4);
     mcrc::build_lds_image4(img.data(), mcrc_dev::kSpanCH);
+    for (uint32_t t = 0; t < 16; ++t) {  // x^(i - 8t): lane-distributed multiply by x^(-8t)
+        const uint32_t xinv = mcrc::xpow8n_inv(t);
+        for (uint32_t i = 0; i < 32; ++i)
+            img[mcrc_dev::kXinvOffset / 4 + t * 32 + i] = mcrc::mulmodp(0x80000000u >> i, xinv);
+    }
     std::vector<uint32_t> xp(3 * 1024 + 16);
     for (uint32_t j = 0; j < 1024; ++j) {
         xp[j] = mcrc::xpow8n(j);
@@ -126,6 +133,17 @@ int init_device(Device &d, int id) {
     HIP_OK(hipMalloc(&d.img, img.size() * 4));
     HIP_OK(hipMemcpy(d.img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
     d.img_k1 = d.img;  // K1 and the span kernels share the CH = 32 image
+    std::vector<uint32_t> sp(512 * 32);
+    for (uint32_t k = 0; k < 256; ++k) {
+        const uint32_t lo = mcrc::xpow8n((uint64_t)mcrc_dev::kSegBytes * k);
+        const uint32_t hi = mcrc::xpow8n((uint64_t)mcrc_dev::kSegBytes * 256 * k);
+        for (uint32_t i = 0; i < 32; ++i) {
+            sp[k * 32 + i] = mcrc::mulmodp(0x80000000u >> i, lo);
+            sp[(256 + k) * 32 + i] = mcrc::mulmodp(0x80000000u >> i, hi);
+        }
+    }
+    HIP_OK(hipMalloc(&d.segpow, sp.size() * 4));
+    HIP_OK(hipMemcpy(d.segpow, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&d.xpow, xp.size() * 4));
     HIP_OK(hipMemcpy(d.xpow, xp.data(), xp.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&d.zero, 64));
@@ -135,11 +153,15 @@ int init_device(Device &d, int id) {
     HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&d.ev0));
     HIP_OK(hipEventCreate(&d.ev1));
-    const void *kernels[] = {
-        (const void *)K1_KERNEL, (const void *)mcrc_dev::k_spans<0>, (const void *)mcrc_dev::k_spans<1>,
+    HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               mcrc_dev::kLdsImage4Bytes));
+    const void *spans[] = {
+        (const void *)mcrc_dev::k_spans<0, false>,
+        (const void *)mcrc_dev::k_spans<0, true>,
+        (const void *)mcrc_dev::k_spans<1, true>,
     };
-    for (const void *k : kernels)
-        HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImage4Bytes));
+    for (const void *k : spans)
+        HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsSpanBytes));
     d.ok = true;
     return CRC32C_OK;
 }
@@ -175,9 +197,12 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
         (void)hipFree(d.nseg);
         (void)hipFree(d.prefix);
         (void)hipFree(d.whole);
+        (void)hipFree(d.irec);
+        (void)hipFree(d.span_acc);
         d.plan_items = 0;
         if (hipMalloc(&d.nseg, n * 4) != hipSuccess || hipMalloc(&d.prefix, n * 4) != hipSuccess ||
-            hipMalloc(&d.whole, n * 8) != hipSuccess)
+            hipMalloc(&d.whole, n * sizeof(mcrc_dev::UnitRec)) != hipSuccess ||
+            hipMalloc(&d.irec, n * sizeof(uint4)) != hipSuccess || hipMalloc(&d.span_acc, n * 4) != hipSuccess)
             return CRC32C_ENOMEM;
         size_t need = 0;
         if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, d.nseg, d.prefix, (int)n) != hipSuccess)
@@ -191,9 +216,8 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
     }
     if (d.plan_units < cap) {
         (void)hipFree(d.units);
-        (void)hipFree(d.seg_raw);
         d.plan_units = 0;
-        if (hipMalloc(&d.units, cap * 8) != hipSuccess || hipMalloc(&d.seg_raw, cap * 4) != hipSuccess)
+        if (hipMalloc(&d.units, cap * sizeof(mcrc_dev::UnitRec)) != hipSuccess)
             return CRC32C_ENOMEM;
         d.plan_units = cap;
     }
@@ -207,8 +231,12 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     const bool identity = MODE == 0 && a.lens == nullptr && a.len <= mcrc_dev::kSegBytes;
     (void)aligned;
     auto spans = [&](const mcrc_dev::SpanArgs &x, int grid) {
-        hipLaunchKernelGGL((mcrc_dev::k_spans<MODE>), dim3(grid), dim3(kBlock), mcrc_dev::kLdsImage4Bytes, st,
-                           x, d.img);
+        if (x.units)
+            hipLaunchKernelGGL((mcrc_dev::k_spans<MODE, true>), dim3(grid), dim3(mcrc_dev::kSpanBlock),
+                               mcrc_dev::kLdsSpanBytes, st, x, d.img);
+        else
+            hipLaunchKernelGGL((mcrc_dev::k_spans<MODE, false>), dim3(grid), dim3(mcrc_dev::kSpanBlock),
+                               mcrc_dev::kLdsSpanBytes, st, x, d.img);
     };
     if (identity) {
         spans(a, grid_for(d, n));
@@ -224,22 +252,23 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     const int g1 = (int)std::min<uint64_t>((n + 255) / 256, 4096);
     HIP_OK(hipMemsetAsync(nvalid, 0xff, 4, st));
     HIP_OK(hipMemsetAsync(nwhole, 0, 4, st));
-    hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nseg);
+    a.span_acc = d.span_acc;
+    hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nseg, d.irec);
     size_t tmp = d.scan_tmp_bytes;
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(d.scan_tmp, tmp, d.nseg, d.prefix, (int)n, st));
-    hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(g1), dim3(256), 0, st, d.nseg, d.prefix, n, d.units, cap, nvalid,
-                       d.whole, nwhole);
+    hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(g1), dim3(256), 0, st, a.base, d.nseg, d.prefix, d.irec, n, d.units,
+                       cap, nvalid, d.whole, nwhole);
     mcrc_dev::SpanArgs u = a;
     u.units = d.units;
     u.nunits = nvalid;
-    u.seg_raw = d.seg_raw;
+    u.span_acc = d.span_acc;
+    u.segpow = d.segpow;
     spans(u, d.cus);
     mcrc_dev::SpanArgs w = a;
     w.units = d.whole;
     w.nunits = nwhole;
     spans(w, d.cus);
-    hipLaunchKernelGGL((mcrc_dev::k_combine<MODE>), dim3(g1), dim3(256), 0, st, u, d.nseg, d.prefix, nvalid,
-                       mcrc::xpow8n(mcrc_dev::kSegBytes));
+    hipLaunchKernelGGL((mcrc_dev::k_combine<MODE>), dim3(g1), dim3(256), 0, st, u, d.nseg, d.prefix, d.irec, nvalid);
     return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
 }
 
@@ -456,8 +485,8 @@ int crc32c_batch(const crc32c_spans *s, unsigned flags, void *stream) {
     return CRC32C_OK;
 }
 
-int crc32c_verify_items(const void *base, uint64_t base_bytes, const uint64_t *item_offsets, uint64_t n,
-                        uint8_t *ok, uint64_t *nbad, unsigned flags, void *stream) {
+int crc32c_verify_items(const void *base, uint64_t base_bytes, uint64_t region_bytes, const uint64_t *item_offsets,
+                        uint64_t n, uint8_t *ok, uint64_t *nbad, unsigned flags, void *stream) {
     if (!base || !item_offsets || !ok || !nbad) return CRC32C_EINVAL;
     Device *d = nullptr;
     int rc = current_device(&d);
@@ -504,6 +533,7 @@ int crc32c_verify_items(const void *base, uint64_t base_bytes, const uint64_t *i
     a.offsets = doffs;
     a.ok = dok;
     a.nbad = d->nbad;
+    a.region = region_bytes;
     a.n = n;
     a.xpow = d->xpow;
     a.zero = d->zero;

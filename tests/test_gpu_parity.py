@@ -168,6 +168,26 @@ def test_verify_long_items(torch):
     assert nbad == 1 and ok[5] == 0
 
 
+def test_verify_region_bound(torch):
+    """A flipped high bit of nbytes makes a header claim a span past its wbuf:
+    with region_bytes = wbuf size it is reported bad without being read; the
+    neighbours are unaffected; without a region it is bad through its CRC."""
+    rng = np.random.default_rng(36)
+    items = [layout.make_item(b"rb%05d" % i, rng.integers(0, 256, 3000 + 37 * i, dtype=np.uint8).tobytes(), cas=i)
+             for i in range(300)]
+    wbuf = 1 << 20
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    soffs, slens = layout.spans_of(buf, offs)
+    layout.store_crcs(buf, offs, oracle.batch(buf, soffs, slens))
+    buf[int(offs[7]) + 32 + 2] ^= 0x08  # nbytes += 512 KiB: crosses the 1 MiB wbuf
+    for region in (wbuf, 0):
+        ok, nbad = mc.verify_items(_dev(torch, buf), _dev(torch, offs.view(np.int64)), region_bytes=region)
+        ok = ok.cpu().numpy()
+        assert nbad == 1 and ok[7] == 0 and ok.sum() == offs.size - 1
+    ok, nbad = mc.verify_items(buf, offs, region_bytes=wbuf)
+    assert nbad == 1 and ok[7] == 0
+
+
 def test_realistic_item_spans_4133(torch):
     """config-1/config-5 geometry: 4133-byte spans at +32 of 4165-byte images."""
     items = [layout.make_item(b"key%07d" % i, np.random.default_rng(i).integers(0, 256, 4096, dtype=np.uint8).tobytes(),
