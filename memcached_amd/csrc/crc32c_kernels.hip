@@ -492,8 +492,10 @@ __device__ __forceinline__ uint32_t keep_before(uint32_t v, int32_t i, uint32_t 
 // Bytes of the 4-byte value x placed at byte offset -d relative to a dword
 // (d = dword position - position of x, in bytes; |d| >= 4 gives 0).
 __device__ __forceinline__ uint32_t place(uint32_t x, int32_t d) {
-    if (d >= 4 || d <= -4) return 0u;
-    return d >= 0 ? x >> (8 * d) : x << (-8 * d);
+    const int32_t c = d < -4 ? -4 : d > 4 ? 4 : d;  // v_med3
+    const uint64_t wide = (uint64_t)x << 32;         // x at bytes 4..7
+    const uint32_t v = (uint32_t)(wide >> (32 + 8 * c));
+    return c == 4 ? 0u : v;                          // (shift 64 would wrap)
 }
 
 // Chains over rows NS..3 of a block, folded to the block's lane value.
@@ -532,7 +534,9 @@ __device__ __forceinline__ void emit(const SpanArgs &a, uint64_t item, uint32_t 
     } else {
         const bool good = sane && crc == aux;
         a.ok[item] = good;
+#ifndef MCRC_ABL_NOHEAD  // (the ablation's CRCs are wrong: do not count them)
         if (!good) atomicAdd(a.nbad, 1ull);
+#endif
     }
 }
 
@@ -625,32 +629,46 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         if (cur.niters) {
             const uint8_t *G = cur.e() - (size_t)kBlockBytes * (cur.niters - k);
             const uint8_t *q0 = G + kSpanCH * li;  // this lane's piece 0 of row 0
-            // head: zero the bytes before p and inject ~crc_in into [p, p+4)
-            // (which can spill into the next piece, possibly in block 1)
+            // head: zero the bytes before p and inject ~crc_in into [p, p+4).
+            // Only the lane owning the piece ph that holds p is touched (and,
+            // when p & 15 > 12, dword 0 of the next piece, which is in block 1
+            // when ph ends block 0).  The owner and the piece follow from
+            // rel = ph - q0: lane li owns it iff 0 <= rel < 4096 and
+            // rel % 1024 < 32; then it is piece (rel >> 10, (rel >> 4) & 1).
+            const uint8_t *ph = (const uint8_t *)((uintptr_t)cur.p & ~(uintptr_t)15);
+            const uint32_t kh = (uint32_t)((uintptr_t)cur.p & 15u);
 #ifdef MCRC_ABL_NOHEAD  // ablation: skip head masking and ~crc_in injection (wrong CRCs)
-            const bool hd = false;
+            const bool hd = false, hd2 = false;
 #else
-            const bool hd = k <= 1 && cur.head();
+            const bool hd = k == 0 && cur.head();
+            const bool hd2 = cur.head() && kh > 12 && cur.Eo >= 4 && (k == 0 || (k == 1 && ph + 16 == G));
 #endif
-            if (__any(hd)) {
-                const uint8_t *ph = (const uint8_t *)((uintptr_t)cur.p & ~(uintptr_t)15);
-                const uint32_t kh = (uint32_t)((uintptr_t)cur.p & 15u);
+            if (__any(hd || hd2)) {
+                const int32_t rel = (int32_t)(ph - q0), rel2 = rel + 16;
+                const auto piece_of = [](int32_t x, bool en) -> int32_t {
+                    return en && x >= 0 && x < (int32_t)kBlockBytes && (x & (kRowBytes - 1)) < (int32_t)kSpanCH
+                               ? 2 * (x >> 10) + ((x >> 4) & 1)
+                               : -1;
+                };
+                const int32_t sel = piece_of(rel, hd), sel2 = piece_of(rel2, hd2);
                 const uint32_t inj = cur.Eo < 4 ? 0u : MODE == 0 ? ~__shfl(cur.raw, (lane & 32u) | 4u, 64) : 0xffffffffu;
+                const int32_t d = -(int32_t)kh;  // ph - p
+                const uint32_t m0 = keep_from(~0u, 0, kh), m1 = keep_from(~0u, 1, kh), m2 = keep_from(~0u, 2, kh),
+                               m3 = keep_from(~0u, 3, kh);
+                const uint32_t i0 = place(inj, d), i1 = place(inj, d + 4), i2 = place(inj, d + 8),
+                               i3 = place(inj, d + 12), s0 = place(inj, d + 16);
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
-                        const uint8_t *q = q0 + r * kRowBytes + 16 * j;
-                        const bool at = hd && q == ph, next = hd && kh > 12 && q == ph + 16;
                         uint4 &v = w.v[r][j];
-                        const int32_t d = (int32_t)(q - cur.p);  // piece start - p (in [-15, 16] when used)
-                        if (at) {
-                            v.x = keep_from(v.x, 0, kh) ^ place(inj, d);
-                            v.y = keep_from(v.y, 1, kh) ^ place(inj, d + 4);
-                            v.z = keep_from(v.z, 2, kh) ^ place(inj, d + 8);
-                            v.w = keep_from(v.w, 3, kh) ^ place(inj, d + 12);
+                        if (sel == 2 * r + j) {
+                            v.x = (v.x & m0) ^ i0;
+                            v.y = (v.y & m1) ^ i1;
+                            v.z = (v.z & m2) ^ i2;
+                            v.w = (v.w & m3) ^ i3;
                         }
-                        if (next) v.x ^= place(inj, d);
+                        if (sel2 == 2 * r + j) v.x ^= s0;
                     }
             }
             // tail: zero the bytes >= E in the span's last piece
@@ -733,10 +751,13 @@ __global__ void k_count(SpanArgs a, uint32_t *nseg, uint4 *irec) {
 // Write the unit records of span i at prefix[i].  Spans whose units would pass
 // `cap` (possible only when spans overlap) are listed in `whole` and processed
 // as one unit each by a second pass; *nvalid = units written before the first
-// such span.
+// such span.  Spans of more than kExpandInline segments are listed in `big`
+// and expanded by k_expand_big, one workgroup per span.
+constexpr uint32_t kExpandInline = 32;
+
 __global__ void k_expand(const uint8_t *base, const uint32_t *nseg, const uint32_t *prefix, const uint4 *irec,
                          uint64_t n, UnitRec *units, uint64_t cap, uint32_t *nvalid, UnitRec *whole,
-                         uint32_t *nwhole) {
+                         uint32_t *nwhole, uint32_t *big, uint32_t *nbig) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t p0 = prefix[i], ns = nseg[i];
@@ -744,12 +765,29 @@ __global__ void k_expand(const uint8_t *base, const uint32_t *nseg, const uint32
         const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
         const bool sane = !(r.y & kInsane);
         if (p0 + ns <= cap) {
-            for (uint32_t s = 0; s < ns; ++s) units[p0 + s] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, s);
+            if (ns > kExpandInline)
+                big[atomicAdd(nbig, 1u)] = (uint32_t)i;
+            else
+                for (uint32_t s = 0; s < ns; ++s) units[p0 + s] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, s);
             if (i + 1 == n) *nvalid = (uint32_t)(p0 + ns);
         } else {
             if (p0 <= cap) atomicMin(nvalid, (uint32_t)p0);
             whole[atomicAdd(nwhole, 1u)] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, kWhole);
         }
+    }
+}
+
+__global__ void k_expand_big(const uint8_t *base, const uint32_t *nseg, const uint32_t *prefix, const uint4 *irec,
+                             UnitRec *units, const uint32_t *big, const uint32_t *nbig) {
+    const uint32_t nb = *nbig;
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t i = big[b];
+        const uint64_t p0 = prefix[i];
+        const uint32_t ns = nseg[i];
+        const uint4 r = irec[i];
+        const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
+        for (uint32_t s = threadIdx.x; s < ns; s += blockDim.x)
+            units[p0 + s] = make_unit(base, off, r.z, r.w, !(r.y & kInsane), i, s);
     }
 }
 

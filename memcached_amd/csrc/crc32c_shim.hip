@@ -84,6 +84,7 @@ struct Device {
     uint32_t *segpow = nullptr;  // rows x^i * x^(8*64Ki*k): k < 256, then k = 256 j
     mcrc_dev::UnitRec *units = nullptr, *whole = nullptr;
     uint4 *irec = nullptr;  // per-span record written by k_count
+    uint32_t *big = nullptr;  // spans expanded by k_expand_big
     void *scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
     uint64_t plan_items = 0, plan_units = 0;
@@ -199,10 +200,12 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
         (void)hipFree(d.whole);
         (void)hipFree(d.irec);
         (void)hipFree(d.span_acc);
+        (void)hipFree(d.big);
         d.plan_items = 0;
         if (hipMalloc(&d.nseg, n * 4) != hipSuccess || hipMalloc(&d.prefix, n * 4) != hipSuccess ||
             hipMalloc(&d.whole, n * sizeof(mcrc_dev::UnitRec)) != hipSuccess ||
-            hipMalloc(&d.irec, n * sizeof(uint4)) != hipSuccess || hipMalloc(&d.span_acc, n * 4) != hipSuccess)
+            hipMalloc(&d.irec, n * sizeof(uint4)) != hipSuccess || hipMalloc(&d.span_acc, n * 4) != hipSuccess ||
+            hipMalloc(&d.big, n * 4) != hipSuccess)
             return CRC32C_ENOMEM;
         size_t need = 0;
         if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, d.nseg, d.prefix, (int)n) != hipSuccess)
@@ -248,16 +251,18 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     const uint64_t cap = std::min<uint64_t>(n + a.base_bytes / mcrc_dev::kSegBytes + 1 + n / 4096, 0xfffffff0ull);
     int rc = ensure_plan(d, n, cap);
     if (rc) return rc;
-    uint32_t *nvalid = d.counters, *nwhole = d.counters + 1;
+    uint32_t *nvalid = d.counters, *nwhole = d.counters + 1, *nbig = d.counters + 2;
     const int g1 = (int)std::min<uint64_t>((n + 255) / 256, 4096);
     HIP_OK(hipMemsetAsync(nvalid, 0xff, 4, st));
-    HIP_OK(hipMemsetAsync(nwhole, 0, 4, st));
+    HIP_OK(hipMemsetAsync(nwhole, 0, 8, st));  // nwhole, nbig
     a.span_acc = d.span_acc;
     hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nseg, d.irec);
     size_t tmp = d.scan_tmp_bytes;
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(d.scan_tmp, tmp, d.nseg, d.prefix, (int)n, st));
     hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(g1), dim3(256), 0, st, a.base, d.nseg, d.prefix, d.irec, n, d.units,
-                       cap, nvalid, d.whole, nwhole);
+                       cap, nvalid, d.whole, nwhole, d.big, nbig);
+    hipLaunchKernelGGL(mcrc_dev::k_expand_big, dim3(1024), dim3(256), 0, st, a.base, d.nseg, d.prefix, d.irec,
+                       d.units, d.big, nbig);
     mcrc_dev::SpanArgs u = a;
     u.units = d.units;
     u.nunits = nvalid;
