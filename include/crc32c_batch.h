@@ -8,6 +8,10 @@
  *                          the read-back CRC of storage.c:172 and
  *                          proxy_internal.c:28 gathered per IO batch
  *                          (extstore.c:853-945).
+ *   crc32c_stamp_items     the spill CRC of storage.c:567 for every item image of
+ *                          a wbuf, written into exptime.
+ *   crc32c_verify_pages    the same over whole pages, walked on the device as
+ *                          storage_compact_readback walks them.
  *   crc32c_verify_items    the read-verify compare of storage.c:159-178 applied
  *                          to every item image of a packed extstore page
  *                          (walk of storage.c:950-960): CRC over
@@ -83,6 +87,29 @@ int crc32c_batch_multi(const crc32c_spans *spans, int ngpus);
 int crc32c_verify_items(const void *base, uint64_t base_bytes, uint64_t region_bytes,
                         const uint64_t *item_offsets, uint64_t n, uint8_t *ok, uint64_t *nbad,
                         unsigned flags, void *stream);
+
+/* Verify whole pages with the walk done on the device: [base, base_bytes) is
+ * a sequence of wbuf_bytes reads, each walked as storage_compact_readback does
+ * (storage.c:950-1070: items packed from the read's start, nkey == 0 ends it,
+ * next item at + ITEM_ntotal, stop when < 48 bytes remain) and every item
+ * verified as crc32c_verify_items does (with region_bytes = wbuf_bytes).
+ * *nitems = items found; the first min(cap, *nitems) offsets and ok flags are
+ * written to offsets[] / ok[] (may be NULL when cap == 0), in walk order. */
+int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_bytes,
+                        uint64_t *offsets, uint8_t *ok, uint64_t cap, uint64_t *nitems,
+                        uint64_t *nbad, unsigned flags, void *stream);
+
+/* Stamp the spill CRC of n item images (storage.c:567, gathered per wbuf
+ * before it is submitted): exptime (bytes 28..31) of image i receives
+ * crc32c(0, image + 32, ITEM_ntotal - 32).  Host or device per flags; with
+ * CRC32C_DEVICE | CRC32C_ASYNC and nbad == NULL the call returns once the
+ * kernels are enqueued on `stream` (the caller fences reads of the wbuf on
+ * that stream).  ok (optional) marks stamped images;
+ * malformed images are left untouched and counted in *nbad.  region_bytes as
+ * for crc32c_verify_items. */
+int crc32c_stamp_items(void *base, uint64_t base_bytes, uint64_t region_bytes,
+                       const uint64_t *item_offsets, uint64_t n, uint8_t *ok, uint64_t *nbad,
+                       unsigned flags, void *stream);
 
 /* Asynchronous form of crc32c_batch for host batches: returns at once with a
  * job handle; crc32c_batch_wait blocks until out[] is filled and frees it. */

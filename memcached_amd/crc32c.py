@@ -7,6 +7,8 @@ include/crc32c_batch.h and run the gfx950 kernels:
 
 * ``batch``        out[i] = crc32c(crc_in[i] or 0, span i)  (storage.c:567, :172)
 * ``verify_items`` stored-CRC check of packed item images (storage.c:160-178)
+* ``stamp_items``  spill CRC written into each image's exptime (storage.c:567)
+* ``verify_pages`` walk + verify whole pages on the device (storage.c:950-1070)
 * ``batch_multi``  host batch split across GPUs by bytes
 
 Host inputs are numpy arrays (or bytes); device inputs are torch tensors on a
@@ -21,7 +23,8 @@ import numpy as np
 from . import _lib
 from ._lib import CRC32C_ALIGNED16, CRC32C_ASYNC, CRC32C_DEVICE, Crc32cError, check, lib
 
-__all__ = ["crc32c", "crc32c_sw", "batch", "verify_items", "batch_multi", "gpu_count", "Crc32cError"]
+__all__ = ["crc32c", "crc32c_sw", "batch", "verify_items", "stamp_items", "verify_pages", "batch_multi", "gpu_count",
+           "Crc32cError"]
 
 
 def _host_buf(data):
@@ -141,3 +144,59 @@ def verify_items(buf, item_offsets, region_bytes=0, stream=None):
                                      ok.ctypes.data, ctypes.byref(nbad), 0, None)
     check(rc, "crc32c_verify_items")
     return ok, int(nbad.value)
+
+
+def stamp_items(buf, item_offsets, region_bytes=0, stream=None):
+    """Write the spill CRC of every item image into its exptime field, in place
+    (storage.c:567 for a whole wbuf at once).  Returns (ok, nbad): ok marks
+    stamped images, nbad counts malformed ones (left untouched)."""
+    dev = _is_torch(buf) and buf.is_cuda
+    nbad = ctypes.c_uint64(0)
+    if dev:
+        import torch
+        n = item_offsets.numel()
+        ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(buf.device).cuda_stream
+        rc = lib.crc32c_stamp_items(buf.data_ptr(), buf.numel() * buf.element_size(), region_bytes,
+                                    item_offsets.data_ptr(), n, ok.data_ptr(), ctypes.byref(nbad), CRC32C_DEVICE,
+                                    stream)
+    else:
+        if not (isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and buf.flags.writeable
+                and buf.flags.c_contiguous):
+            raise TypeError("stamp_items needs a writable contiguous uint8 numpy array (stamped in place)")
+        offs = np.ascontiguousarray(item_offsets, dtype=np.uint64)
+        ok = np.empty(offs.size, dtype=np.uint8)
+        rc = lib.crc32c_stamp_items(buf.ctypes.data, buf.size, region_bytes, offs.ctypes.data, offs.size,
+                                    ok.ctypes.data, ctypes.byref(nbad), 0, None)
+    check(rc, "crc32c_stamp_items")
+    return ok, int(nbad.value)
+
+
+def verify_pages(buf, wbuf_bytes, stream=None):
+    """Walk every wbuf-sized read of ``buf`` on the device and verify each
+    item found.  Returns (item offsets, ok flags, nbad) in walk order."""
+    dev = _is_torch(buf) and buf.is_cuda
+    nitems, nbad = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    if dev:
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(buf.device).cuda_stream
+        nbytes = buf.numel() * buf.element_size()
+        check(lib.crc32c_verify_pages(buf.data_ptr(), nbytes, wbuf_bytes, None, None, 0, ctypes.byref(nitems),
+                                      ctypes.byref(nbad), CRC32C_DEVICE, stream), "crc32c_verify_pages")
+        n = nitems.value
+        offs = torch.empty(n, dtype=torch.int64, device=buf.device)
+        ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
+        check(lib.crc32c_verify_pages(buf.data_ptr(), nbytes, wbuf_bytes, offs.data_ptr(), ok.data_ptr(), n,
+                                      ctypes.byref(nitems), ctypes.byref(nbad), CRC32C_DEVICE, stream),
+              "crc32c_verify_pages")
+        return offs, ok, int(nbad.value)
+    buf = _host_buf(buf)
+    cap = buf.size // 50 + 1  # an image is at least 50 bytes
+    offs = np.empty(cap, np.uint64)
+    ok = np.empty(cap, np.uint8)
+    check(lib.crc32c_verify_pages(buf.ctypes.data, buf.size, wbuf_bytes, offs.ctypes.data, ok.ctypes.data, cap,
+                                  ctypes.byref(nitems), ctypes.byref(nbad), 0, None), "crc32c_verify_pages")
+    n = nitems.value
+    return offs[:n], ok[:n], int(nbad.value)

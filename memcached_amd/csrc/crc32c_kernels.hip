@@ -4,12 +4,15 @@
 //     stride, len = R*LPI*CH (extstore spill batches of one slab class;
 //     BASELINE configs 2 and 4).  Replaces N calls of crc32c(0, item, len),
 //     crc32c_hw (crc32c.c:161-246) reached from storage.c:567.
-// K2  k_spans<UNALIGNED, MODE=0>: any offsets, lengths and alignment; one
-//     32-lane group per span (configs 3 and 5, storage.c:172 read-back spans).
-// K3  k_spans<true, MODE=1>: verify packed item images in extstore pages: the
+// K2  k_spans<MODE=0, UNITS>: any offsets, lengths and alignment; one 32-lane
+//     group per work unit of <= 64 KiB (configs 3 and 5, storage.c:172
+//     read-back spans).
+// K3  k_spans<MODE=1>: verify packed item images in extstore pages: the
 //     span [off+32, off+ITEM_ntotal) is checked against the CRC stored in the
 //     item's exptime field (storage.c:160-178 over the page walk of
 //     storage.c:950-960).
+//     k_spans<MODE=2>: stamp: the same spans, the CRC written into exptime
+//     (the spill CRC of storage.c:567, batched per wbuf).
 //
 // See crc32c_device.h for the lane-group work model and LDS table layouts.
 #include "crc32c_device.h"
@@ -530,17 +533,34 @@ __device__ __forceinline__ uint32_t xpow8_dev(const uint32_t *xp, uint32_t len) 
     return r;
 }
 
-// Store (MODE 0) or compare (MODE 1) the final CRC of span `item`.
+// Store (MODE 0), compare (MODE 1) or stamp (MODE 2) the final CRC of span
+// `item`, which starts at p.  Stamp writes the spill CRC into the image's
+// exptime field, bytes 28..31 = p - 4 (storage.c:567), or into out[] when the
+// caller stages the images (host path); ok[] (if any) marks stamped images.
 template <int MODE>
-__device__ __forceinline__ void emit(const SpanArgs &a, uint64_t item, uint32_t crc, uint32_t aux, bool sane) {
+__device__ __forceinline__ void emit(const SpanArgs &a, uint64_t item, uint32_t crc, uint32_t aux, bool sane,
+                                     const uint8_t *p) {
     if (MODE == 0) {
         a.out[item] = crc;
-    } else {
+    } else if (MODE == 1) {
         const bool good = sane && crc == aux;
         a.ok[item] = good;
 #ifndef MCRC_ABL_NOHEAD  // (the ablation's CRCs are wrong: do not count them)
         if (!good) atomicAdd(a.nbad, 1ull);
 #endif
+    } else {
+        if (a.ok) a.ok[item] = sane;
+        if (!sane) {
+            atomicAdd(a.nbad, 1ull);
+        } else if (a.out) {
+            a.out[item] = crc;
+        } else {
+            uint8_t *x = const_cast<uint8_t *>(p) - 4;
+            x[0] = (uint8_t)crc;
+            x[1] = (uint8_t)(crc >> 8);
+            x[2] = (uint8_t)(crc >> 16);
+            x[3] = (uint8_t)(crc >> 24);
+        }
     }
 }
 
@@ -559,7 +579,7 @@ __device__ __forceinline__ void finalize(const SpanArgs &a, uint64_t item, uint3
     uint32_t v = raw_v;
     if (span_len < 4) v ^= short_init<MODE>(a, aux, span_len, t);
     if (t) v = mulmodp_dev(v, a.xpow[3072 + t]);
-    emit<MODE>(a, item, ~v, aux, sane);
+    emit<MODE>(a, item, ~v, aux, sane, p);
 }
 
 // v0 (lane 0 of the group) times the element whose row `row` holds
@@ -710,7 +730,7 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
                     const uint32_t item = __shfl(cur.raw, (lane & 32u) | 5u, 64);
                     if (li == 0 && cur.Eo < 4) raw ^= short_init<MODE>(a, aux, cur.Eo, t);
                     const uint32_t v = mul_xinv_group(raw, t, li);
-                    if (li == 0) emit<MODE>(a, item, ~v, aux, cur.sane());
+                    if (li == 0) emit<MODE>(a, item, ~v, aux, cur.sane(), cur.p);
                 } else {
                     // segment s of nseg: raw_v(span) gets M_{64Ki * (nseg-1-s)}(raw)
                     const uint32_t k = __shfl(cur.raw, (lane & 32u) | 7u, 64);
@@ -807,6 +827,34 @@ __global__ void k_combine(SpanArgs a, const uint32_t *nseg, const uint32_t *pref
         const uint4 r = irec[i];
         const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
         finalize<MODE>(a, i, a.span_acc[i], r.w, a.base + off, r.z, !(r.y & kInsane));
+    }
+}
+
+// Device-side page walk (storage_compact_readback, storage.c:950-1070): the
+// buffer is a sequence of wbuf-sized reads; in each, items are packed from
+// offset 0, nkey == 0 ends the wbuf, the next item is at + ITEM_ntotal, and the
+// walk stops when fewer than sizeof(item) = 48 bytes remain.  One thread per
+// wbuf (the walk is a dependent chain).  Pass 1 (prefix == nullptr) counts the
+// items of every wbuf; pass 2 writes their offsets at prefix[w].
+__global__ void k_walk(const uint8_t *base, uint64_t bytes, uint64_t wbuf, uint64_t nw, uint32_t *cnt,
+                       const uint32_t *prefix, uint64_t *offs) {
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nw;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t start = w * wbuf, size = bytes - start < wbuf ? bytes - start : wbuf;
+        uint64_t off = 0;
+        uint32_t c = 0;
+        const uint64_t o0 = prefix ? prefix[w] : 0;
+        while (off + 48 <= size) {
+            const uint8_t *it = base + start + off;
+            const uint32_t nkey = it[41];
+            if (nkey == 0) break;  // zeroed tail of the wbuf
+            const uint32_t nbytes = ld_u32_unaligned(it + 32);
+            const uint32_t flags = it[38] | (it[39] << 8);
+            if (prefix) offs[o0 + c] = start + off;
+            ++c;
+            off += 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) + ((flags & 2u) ? 8 : 0);
+        }
+        if (!prefix) cnt[w] = c;
     }
 }
 

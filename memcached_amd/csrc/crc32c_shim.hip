@@ -88,7 +88,24 @@ struct Device {
     void *scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
     uint64_t plan_items = 0, plan_units = 0;
+    // grow-only scratch for the page walk and staged item batches
+    struct Scratch {
+        void *p = nullptr;
+        size_t bytes = 0;
+    } scratch[7];
+    void *grow(int slot, size_t bytes) {
+        Scratch &s = scratch[slot];
+        if (s.bytes < bytes) {
+            if (s.p) (void)hipFree(s.p);
+            s.p = nullptr;
+            s.bytes = 0;
+            if (hipMalloc(&s.p, bytes) != hipSuccess) return nullptr;
+            s.bytes = bytes;
+        }
+        return s.p;
+    }
 };
+enum { kScrWalkCnt, kScrWalkCnt1, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage };
 
 std::mutex g_dev_mu;
 std::vector<std::unique_ptr<Device>> g_devs;
@@ -160,6 +177,7 @@ int init_device(Device &d, int id) {
         (const void *)mcrc_dev::k_spans<0, false>,
         (const void *)mcrc_dev::k_spans<0, true>,
         (const void *)mcrc_dev::k_spans<1, true>,
+        (const void *)mcrc_dev::k_spans<2, true>,
     };
     for (const void *k : spans)
         HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsSpanBytes));
@@ -441,6 +459,97 @@ int run_host_batch(Device &d, const crc32c_spans &s) {
     return CRC32C_OK;
 }
 
+// Item-image batches (verify: MODE 1, stamp: MODE 2) over a packed buffer of
+// item images at item_offsets.  Host buffers are staged through device memory;
+// stamp on a host buffer brings back only the CRCs and writes them into the
+// images' exptime fields here.
+template <int MODE>
+int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const uint64_t *item_offsets, uint64_t n,
+                uint8_t *ok, uint64_t *nbad, unsigned flags, void *stream) {
+    if (!base || !item_offsets || (MODE == 1 && !ok)) return CRC32C_EINVAL;
+    Device *d = nullptr;
+    int rc = current_device(&d);
+    if (rc) return rc;
+    if (n == 0) {
+        if (nbad) *nbad = 0;
+        return CRC32C_OK;
+    }
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t st = (hipStream_t)stream;  // NULL: the default stream
+    const bool dev = flags & CRC32C_DEVICE;
+    const uint8_t *dbase = (const uint8_t *)base;
+    const uint64_t *doffs = item_offsets;
+    uint8_t *dok = ok;
+    uint32_t *dcrc = nullptr;
+    std::vector<void *> tmp;
+    auto dalloc = [&](size_t bytes) -> void * {
+        void *p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        tmp.push_back(p);
+        return p;
+    };
+    auto cleanup = [&]() {
+        for (void *p : tmp) (void)hipFree(p);
+    };
+    if (!dev) {
+        uint8_t *b = (uint8_t *)dalloc(base_bytes);
+        uint64_t *o = (uint64_t *)dalloc(n * 8);
+        dok = (uint8_t *)dalloc(n);
+        if (MODE == 2) dcrc = (uint32_t *)dalloc(n * 4);
+        if (!b || !o || !dok || (MODE == 2 && !dcrc)) {
+            cleanup();
+            return CRC32C_ENOMEM;
+        }
+        if (hipMemcpyAsync(b, base, base_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(o, item_offsets, n * 8, hipMemcpyHostToDevice, st) != hipSuccess) {
+            cleanup();
+            return CRC32C_EHIP;
+        }
+        dbase = b;
+        doffs = o;
+    }
+    mcrc_dev::SpanArgs a{};
+    a.base = dbase;
+    a.base_bytes = base_bytes;
+    a.offsets = doffs;
+    a.ok = dok;
+    a.out = dcrc;  // stamp: nullptr = write into the images
+    a.nbad = d->nbad;
+    a.n = n;
+    a.xpow = d->xpow;
+    a.zero = d->zero;
+    a.region = region_bytes;
+    (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
+    rc = launch_units<MODE>(*d, a, false, st);
+    if (rc) {
+        cleanup();
+        return rc;
+    }
+    if (dev && (flags & CRC32C_ASYNC) && !nbad) return CRC32C_OK;  // device, fire and forget
+    unsigned long long bad = 0;
+    std::vector<uint32_t> crcs;
+    std::vector<uint8_t> oks;
+    bool fail = hipMemcpyAsync(&bad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st) != hipSuccess;
+    if (!dev && MODE == 1) fail = fail || hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, st) != hipSuccess;
+    if (!dev && MODE == 2) {
+        crcs.resize(n);
+        oks.resize(n);
+        fail = fail || hipMemcpyAsync(crcs.data(), dcrc, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipMemcpyAsync(oks.data(), dok, n, hipMemcpyDeviceToHost, st) != hipSuccess;
+    }
+    fail = fail || hipStreamSynchronize(st) != hipSuccess;
+    cleanup();
+    if (fail) return CRC32C_EHIP;
+    if (!dev && MODE == 2) {
+        uint8_t *b = (uint8_t *)base;
+        for (uint64_t i = 0; i < n; ++i)
+            if (oks[i]) memcpy(b + item_offsets[i] + 28, &crcs[i], 4);  // exptime (storage.c:567)
+        if (ok) memcpy(ok, oks.data(), n);
+    }
+    if (nbad) *nbad = bad;
+    return CRC32C_OK;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -492,68 +601,88 @@ int crc32c_batch(const crc32c_spans *s, unsigned flags, void *stream) {
 
 int crc32c_verify_items(const void *base, uint64_t base_bytes, uint64_t region_bytes, const uint64_t *item_offsets,
                         uint64_t n, uint8_t *ok, uint64_t *nbad, unsigned flags, void *stream) {
-    if (!base || !item_offsets || !ok || !nbad) return CRC32C_EINVAL;
+    if (!nbad) return CRC32C_EINVAL;
+    return item_images<1>(const_cast<void *>(base), base_bytes, region_bytes, item_offsets, n, ok, nbad,
+                          flags & ~(unsigned)CRC32C_ASYNC, stream);
+}
+
+int crc32c_stamp_items(void *base, uint64_t base_bytes, uint64_t region_bytes, const uint64_t *item_offsets,
+                       uint64_t n, uint8_t *ok, uint64_t *nbad, unsigned flags, void *stream) {
+    return item_images<2>(base, base_bytes, region_bytes, item_offsets, n, ok, nbad, flags, stream);
+}
+
+int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_bytes, uint64_t *offsets, uint8_t *ok,
+                        uint64_t cap, uint64_t *nitems, uint64_t *nbad, unsigned flags, void *stream) {
+    if (!base || !wbuf_bytes || !nitems || !nbad || (cap && (!offsets || !ok))) return CRC32C_EINVAL;
     Device *d = nullptr;
     int rc = current_device(&d);
     if (rc) return rc;
-    if (n == 0) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t st = (hipStream_t)stream;
+    const bool dev = flags & CRC32C_DEVICE;
+    const uint64_t nw = (base_bytes + wbuf_bytes - 1) / wbuf_bytes;
+    if (nw == 0 || nw >= 0x7fffffffull) {
+        *nitems = *nbad = 0;
+        return nw ? CRC32C_EINVAL : CRC32C_OK;
+    }
+    const uint8_t *dbase = (const uint8_t *)base;
+    if (!dev) {
+        uint8_t *b = (uint8_t *)d->grow(kScrStage, base_bytes);
+        if (!b) return CRC32C_ENOMEM;
+        HIP_OK(hipMemcpyAsync(b, base, base_bytes, hipMemcpyHostToDevice, st));
+        dbase = b;
+    }
+    uint32_t *cnt = (uint32_t *)d->grow(kScrWalkCnt, nw * 4);
+    uint32_t *prefix = (uint32_t *)d->grow(kScrWalkPrefix, (nw + 1) * 4);
+    size_t tmp = 0;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, prefix, (int)nw + 1));
+    void *scan = d->grow(kScrWalkScan, tmp);
+    if (!cnt || !prefix || !scan) return CRC32C_ENOMEM;
+    const int gw = (int)std::min<uint64_t>((nw + 255) / 256, 1024);
+    hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(256), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt,
+                       (const uint32_t *)nullptr, (uint64_t *)nullptr);
+    // prefix[nw] = total: scan nw + 1 counts with a zero appended
+    uint32_t *cnt1 = (uint32_t *)d->grow(kScrWalkCnt1, (nw + 1) * 4);
+    if (!cnt1) return CRC32C_ENOMEM;
+    HIP_OK(hipMemcpyAsync(cnt1, cnt, nw * 4, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipMemsetAsync(cnt1 + nw, 0, 4, st));
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(scan, tmp, cnt1, prefix, (int)nw + 1, st));
+    uint32_t total = 0;
+    HIP_OK(hipMemcpyAsync(&total, prefix + nw, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    *nitems = total;
+    if (total == 0) {
         *nbad = 0;
         return CRC32C_OK;
     }
-    std::lock_guard<std::mutex> lk(d->mu);
-    hipStream_t st = (hipStream_t)stream;  // NULL: the default stream
-    const bool dev = flags & CRC32C_DEVICE;
-    const uint8_t *dbase = (const uint8_t *)base;
-    const uint64_t *doffs = item_offsets;
-    uint8_t *dok = ok;
-    std::vector<void *> tmp;
-    auto dalloc = [&](size_t bytes) -> void * {
-        void *p = nullptr;
-        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-        tmp.push_back(p);
-        return p;
-    };
-    auto cleanup = [&]() {
-        for (void *p : tmp) (void)hipFree(p);
-    };
-    if (!dev) {
-        uint8_t *b = (uint8_t *)dalloc(base_bytes);
-        uint64_t *o = (uint64_t *)dalloc(n * 8);
-        dok = (uint8_t *)dalloc(n);
-        if (!b || !o || !dok) {
-            cleanup();
-            return CRC32C_ENOMEM;
-        }
-        if (hipMemcpyAsync(b, base, base_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
-            hipMemcpyAsync(o, item_offsets, n * 8, hipMemcpyHostToDevice, st) != hipSuccess) {
-            cleanup();
-            return CRC32C_EHIP;
-        }
-        dbase = b;
-        doffs = o;
-    }
+    const bool direct = dev && cap >= total;  // caller's device arrays take the results
+    uint64_t *doffs = direct ? offsets : (uint64_t *)d->grow(kScrWalkOffs, (size_t)total * 8);
+    uint8_t *dok = direct ? ok : (uint8_t *)d->grow(kScrWalkOk, total);
+    if (!doffs || !dok) return CRC32C_ENOMEM;
+    hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(256), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt,
+                       (const uint32_t *)prefix, doffs);
     mcrc_dev::SpanArgs a{};
     a.base = dbase;
     a.base_bytes = base_bytes;
     a.offsets = doffs;
     a.ok = dok;
     a.nbad = d->nbad;
-    a.region = region_bytes;
-    a.n = n;
+    a.n = total;
     a.xpow = d->xpow;
     a.zero = d->zero;
-    (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
+    a.region = wbuf_bytes;
+    HIP_OK(hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st));
     rc = launch_units<1>(*d, a, false, st);
-    if (rc) {
-        cleanup();
-        return rc;
-    }
+    if (rc) return rc;
     unsigned long long bad = 0;
-    bool fail = hipMemcpyAsync(&bad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st) != hipSuccess;
-    if (!dev) fail = fail || hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, st) != hipSuccess;
-    fail = fail || hipStreamSynchronize(st) != hipSuccess;
-    cleanup();
-    if (fail) return CRC32C_EHIP;
+    HIP_OK(hipMemcpyAsync(&bad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st));
+    const uint64_t k = std::min<uint64_t>(cap, total);
+    if (!direct && k) {
+        const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        HIP_OK(hipMemcpyAsync(offsets, doffs, k * 8, kind, st));
+        HIP_OK(hipMemcpyAsync(ok, dok, k, kind, st));
+    }
+    HIP_OK(hipStreamSynchronize(st));
     *nbad = bad;
     return CRC32C_OK;
 }

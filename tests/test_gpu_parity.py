@@ -188,6 +188,88 @@ def test_verify_region_bound(torch):
     assert nbad == 1 and ok[7] == 0
 
 
+def test_stamp_items(torch):
+    """Write path: the spill CRC of every image of a wbuf written into exptime
+    (storage.c:567), device and host, equals the oracle's; the stamped page
+    then verifies clean; a header crossing its wbuf is left unstamped."""
+    rng = np.random.default_rng(37)
+    items = [layout.make_item(b"st%06d" % i, rng.integers(0, 256, int(rng.integers(0, 9000)), dtype=np.uint8).tobytes(),
+                              cas=i + 1) for i in range(900)]
+    wbuf = 1 << 20
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    soffs, slens = layout.spans_of(buf, offs)
+    want = buf.copy()
+    layout.store_crcs(want, offs, oracle.batch(buf, soffs, slens))
+    d = _dev(torch, buf)
+    ok, nbad = mc.stamp_items(d, _dev(torch, offs.view(np.int64)), region_bytes=wbuf)
+    assert nbad == 0 and ok.cpu().numpy().all()
+    np.testing.assert_array_equal(d.cpu().numpy(), want)
+    h = buf.copy()
+    ok, nbad = mc.stamp_items(h, offs, region_bytes=wbuf)
+    assert nbad == 0 and ok.all()
+    np.testing.assert_array_equal(h, want)
+    ok, nbad = mc.verify_items(h, offs, region_bytes=wbuf)
+    assert nbad == 0 and ok.all()
+    # async device stamp on the default stream, fenced by a synchronize
+    d = _dev(torch, buf)
+    import ctypes
+    doffs = _dev(torch, offs.view(np.int64))
+    _lib.check(_lib.lib.crc32c_stamp_items(d.data_ptr(), d.numel(), wbuf, doffs.data_ptr(), offs.size, None, None,
+                                           _lib.CRC32C_DEVICE | _lib.CRC32C_ASYNC,
+                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d.cpu().numpy(), want)
+    # malformed: nbytes claims a span past the wbuf -> not stamped, counted
+    bad = buf.copy()
+    bad[int(offs[11]) + 32 + 2] ^= 0x10
+    ok, nbad = mc.stamp_items(bad, offs, region_bytes=wbuf)
+    assert nbad == 1 and ok[11] == 0 and ok.sum() == offs.size - 1
+    assert bytes(bad[int(offs[11]) + 28:int(offs[11]) + 32]) == b"\0\0\0\0"
+
+
+def _walk(buf, wbuf):
+    """storage_compact_readback's walk (storage.c:950-1070), one read per wbuf."""
+    offs = []
+    for start in range(0, buf.size, wbuf):
+        size, off = min(wbuf, buf.size - start), 0
+        while off + 48 <= size and buf[start + off + 41] != 0:
+            offs.append(start + off)
+            off += layout.ntotal_of(buf, start + off)
+    return np.asarray(offs, np.uint64)
+
+
+def test_verify_pages_device_walk(torch):
+    """Pages walked on the device: same items as the reference walk, every
+    stored CRC checked, corrupted items (and a zeroed nkey, which ends its
+    wbuf's walk early) reported exactly."""
+    rng = np.random.default_rng(38)
+    items = [layout.make_item(b"pg%06d" % i, rng.integers(0, 256, int(rng.integers(0, 20000)), dtype=np.uint8).tobytes(),
+                              cas=i + 1) for i in range(1500)]
+    wbuf = 1 << 20
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    ok, nbad = mc.stamp_items(buf, offs, region_bytes=wbuf)
+    assert nbad == 0
+    np.testing.assert_array_equal(_walk(buf, wbuf), offs)
+    for dev in (True, False):
+        got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, buf) if dev else buf, wbuf)
+        got_offs = got_offs.cpu().numpy().astype(np.uint64) if dev else got_offs
+        got_ok = got_ok.cpu().numpy() if dev else got_ok
+        np.testing.assert_array_equal(got_offs, offs)
+        assert nbad == 0 and got_ok.all()
+    victims = [3, 700, 1499]
+    for v in victims:
+        o = int(offs[v])
+        buf[o + 32 + int(rng.integers(16, layout.ntotal_of(buf, o) - 32))] ^= 0x40
+    buf[int(offs[900]) + 41] = 0  # nkey == 0: the walk of this wbuf ends here
+    want = _walk(buf, wbuf)
+    assert want.size < offs.size
+    got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, buf), wbuf)
+    np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), want)
+    bad_offs = sorted(int(x) for x in got_offs.cpu().numpy()[got_ok.cpu().numpy() == 0])
+    assert bad_offs == sorted(int(offs[v]) for v in victims if int(offs[v]) in set(want.tolist()))
+    assert nbad == len(bad_offs)
+
+
 def test_realistic_item_spans_4133(torch):
     """config-1/config-5 geometry: 4133-byte spans at +32 of 4165-byte images."""
     items = [layout.make_item(b"key%07d" % i, np.random.default_rng(i).integers(0, 256, 4096, dtype=np.uint8).tobytes(),
