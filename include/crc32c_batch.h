@@ -10,6 +10,8 @@
  *                          (extstore.c:853-945).
  *   crc32c_stamp_items     the spill CRC of storage.c:567 for every item image of
  *                          a wbuf, written into exptime.
+ *   crc32c_batch_chains    the chained CRC of chunked items over iov lists
+ *                          (storage.c:163-170).
  *   crc32c_verify_pages    the same over whole pages, walked on the device as
  *                          storage_compact_readback walks them.
  *   crc32c_verify_items    the read-verify compare of storage.c:159-178 applied
@@ -87,6 +89,16 @@ int crc32c_batch_multi(const crc32c_spans *spans, int ngpus);
 int crc32c_verify_items(const void *base, uint64_t base_bytes, uint64_t region_bytes,
                         const uint64_t *item_offsets, uint64_t n, uint8_t *ok, uint64_t *nbad,
                         unsigned flags, void *stream);
+
+/* Chained CRCs over iov lists: the chunked-item read verify of
+ * storage.c:163-170, where crc = crc32c(0, hdr + 32, hdr_len - 32) and then
+ * crc = crc32c(crc, chunk_x, len_x) for every chunk.  iovs describes every
+ * iov of every chain (crc_in must be NULL; iovs->out receives each iov's own
+ * CRC and must hold iovs->n entries); chain c is iovs [chain_first[c],
+ * chain_first[c+1]) (nchains + 1 entries) and out[c] its chained CRC.  All
+ * arrays are host or device memory per flags, as for crc32c_batch. */
+int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, uint64_t nchains,
+                        uint32_t *out, unsigned flags, void *stream);
 
 /* Verify whole pages with the walk done on the device: [base, base_bytes) is
  * a sequence of wbuf_bytes reads, each walked as storage_compact_readback does

@@ -9,6 +9,7 @@ include/crc32c_batch.h and run the gfx950 kernels:
 * ``verify_items`` stored-CRC check of packed item images (storage.c:160-178)
 * ``stamp_items``  spill CRC written into each image's exptime (storage.c:567)
 * ``verify_pages`` walk + verify whole pages on the device (storage.c:950-1070)
+* ``batch_chains`` chained CRCs of chunked items over iov lists (storage.c:163-170)
 * ``batch_multi``  host batch split across GPUs by bytes
 
 Host inputs are numpy arrays (or bytes); device inputs are torch tensors on a
@@ -23,7 +24,7 @@ import numpy as np
 from . import _lib
 from ._lib import CRC32C_ALIGNED16, CRC32C_ASYNC, CRC32C_DEVICE, Crc32cError, check, lib
 
-__all__ = ["crc32c", "crc32c_sw", "batch", "verify_items", "stamp_items", "verify_pages", "batch_multi", "gpu_count",
+__all__ = ["crc32c", "crc32c_sw", "batch", "verify_items", "stamp_items", "verify_pages", "batch_chains", "batch_multi", "gpu_count",
            "Crc32cError"]
 
 
@@ -200,3 +201,30 @@ def verify_pages(buf, wbuf_bytes, stream=None):
                                   ctypes.byref(nitems), ctypes.byref(nbad), 0, None), "crc32c_verify_pages")
     n = nitems.value
     return offs[:n], ok[:n], int(nbad.value)
+
+
+def batch_chains(buf, offsets, lens, chain_first, stream=None):
+    """Chained CRC per iov list: chain c covers iovs [chain_first[c],
+    chain_first[c+1]) of the spans (offsets[i], lens[i]) of ``buf`` and gets
+    crc32c(...crc32c(crc32c(0, iov_a), iov_a+1)..., iov_b-1)."""
+    dev = _is_torch(buf) and buf.is_cuda
+    n, nchains = len(offsets), len(chain_first) - 1
+    if dev:
+        import torch
+        iov_out = torch.empty(n, dtype=torch.int32, device=buf.device)
+        out = torch.empty(nchains, dtype=torch.int32, device=buf.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(buf.device).cuda_stream
+        base_bytes = buf.numel() * buf.element_size()
+    else:
+        buf = _host_buf(buf)
+        base_bytes = buf.size
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        chain_first = np.ascontiguousarray(chain_first, dtype=np.uint64)
+        iov_out = np.empty(n, dtype=np.uint32)
+        out = np.empty(nchains, dtype=np.uint32)
+    s = _lib.Spans(_ptr(buf), base_bytes, _ptr(offsets), 0, _ptr(lens), 0, None, _ptr(iov_out), n)
+    check(lib.crc32c_batch_chains(ctypes.byref(s), _ptr(chain_first), nchains, _ptr(out),
+                                  CRC32C_DEVICE if dev else 0, stream if dev else None), "crc32c_batch_chains")
+    return out

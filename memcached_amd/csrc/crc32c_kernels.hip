@@ -830,6 +830,26 @@ __global__ void k_combine(SpanArgs a, const uint32_t *nseg, const uint32_t *pref
     }
 }
 
+// Chained CRC over an iov list (the chunked-item read verify of
+// storage.c:163-170: crc = crc32c(0, iov0 + 32, ...), then
+// crc = crc32c(crc, iov_x) for every chunk).  Given crc_i = crc32c(0, iov_i),
+// crc32c(c, B) = crc32c(0, B) ^ M_|B|(c), so chain c folds
+//   acc = M_{len_i}(acc) ^ crc_i   over its iovs [first[c], first[c+1]).
+// One thread per chain.
+__global__ void k_chain(const uint32_t *iov_crc, const uint32_t *lens, uint32_t len, const uint64_t *first,
+                        uint64_t nchains, uint32_t *out, const uint32_t *xpow) {
+    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nchains;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t acc = 0;
+        for (uint64_t i = first[c]; i < first[c + 1]; ++i) {
+            const uint32_t l = lens ? lens[i] : len;
+            if (acc) acc = mulmodp_dev(acc, xpow8_dev(xpow, l));
+            acc ^= iov_crc[i];
+        }
+        out[c] = acc;
+    }
+}
+
 // Device-side page walk (storage_compact_readback, storage.c:950-1070): the
 // buffer is a sequence of wbuf-sized reads; in each, items are packed from
 // offset 0, nkey == 0 ends the wbuf, the next item is at + ITEM_ntotal, and the

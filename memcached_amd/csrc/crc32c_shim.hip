@@ -69,7 +69,21 @@ struct Device {
     unsigned long long *nbad = nullptr;
     hipStream_t stream = nullptr, copy = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::mutex mu;              // serialises host batches on this device
+    std::mutex mu;              // serialises every entry point on this device
+    // Shared device scratch (plan buffers, nbad, walk buffers) is owned in
+    // stream order: a launch on stream B waits for the last use on stream A.
+    hipEvent_t busy = nullptr;
+    hipStream_t busy_stream = nullptr;
+    bool busy_valid = false;
+    void acquire(hipStream_t st) {
+        if (busy_valid && busy_stream != st) (void)hipStreamWaitEvent(st, busy, 0);
+    }
+    void release(hipStream_t st) {
+        if (hipEventRecord(busy, st) == hipSuccess) {
+            busy_stream = st;
+            busy_valid = true;
+        }
+    }
     // host-batch staging: two device slots + two pinned slots
     uint8_t *dbuf[2] = {nullptr, nullptr};
     uint8_t *pin[2] = {nullptr, nullptr};
@@ -171,6 +185,7 @@ int init_device(Device &d, int id) {
     HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&d.ev0));
     HIP_OK(hipEventCreate(&d.ev1));
+    HIP_OK(hipEventCreateWithFlags(&d.busy, hipEventDisableTiming));
     HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL, hipFuncAttributeMaxDynamicSharedMemorySize,
                                mcrc_dev::kLdsImage4Bytes));
     const void *spans[] = {
@@ -384,6 +399,12 @@ constexpr uint64_t kSlotItems = 1ull << 20;
 int run_host_batch(Device &d, const crc32c_spans &s) {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_OK(hipSetDevice(d.id));
+    d.acquire(d.stream);
+    d.acquire(d.copy);
+    struct Release {
+        Device &d;
+        ~Release() { d.release(d.stream); }
+    } release_on_exit{d};
     if (s.n == 0) return CRC32C_OK;
     for (uint64_t i = 1; i < s.n; ++i)
         if (span_off(s, i) < span_off(s, i - 1)) return CRC32C_EINVAL;
@@ -519,8 +540,10 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
     a.xpow = d->xpow;
     a.zero = d->zero;
     a.region = region_bytes;
+    d->acquire(st);
     (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
     rc = launch_units<MODE>(*d, a, false, st);
+    d->release(st);
     if (rc) {
         cleanup();
         return rc;
@@ -589,13 +612,68 @@ int crc32c_batch(const crc32c_spans *s, unsigned flags, void *stream) {
     // the kernel is ordered after whatever produced the buffers there.
     hipStream_t st = (hipStream_t)stream;
     const bool timed = !(flags & CRC32C_ASYNC);
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->acquire(st);
     if (timed) HIP_OK(hipEventRecord(d->ev0, st));
     rc = enqueue_device(*d, *s, flags, st);
+    d->release(st);
     if (rc) return rc;
     if (!timed) return CRC32C_OK;
     HIP_OK(hipEventRecord(d->ev1, st));
     HIP_OK(hipEventSynchronize(d->ev1));
     (void)hipEventElapsedTime(&g_last_kernel_ms, d->ev0, d->ev1);
+    return CRC32C_OK;
+}
+
+int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, uint64_t nchains, uint32_t *out,
+                        unsigned flags, void *stream) {
+    if (!iovs || !chain_first || (nchains && !out) || iovs->crc_in) return CRC32C_EINVAL;
+    if (nchains == 0) return CRC32C_OK;
+    Device *d = nullptr;
+    int rc = current_device(&d);
+    if (rc) return rc;
+    const bool dev = flags & CRC32C_DEVICE;
+    if (!dev) {  // per-iov CRCs through the staged host path, then the fold on the device
+        for (uint64_t c = 0; c < nchains; ++c)
+            if (chain_first[c + 1] < chain_first[c] || chain_first[c + 1] > iovs->n) return CRC32C_EINVAL;
+        rc = run_host_batch(*d, *iovs);
+        if (rc) return rc;
+    }
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t st = dev ? (hipStream_t)stream : d->stream;
+    d->acquire(st);
+    struct Release {
+        Device *d;
+        hipStream_t st;
+        ~Release() { d->release(st); }
+    } release_on_exit{d, st};
+    const uint32_t *crcs = iovs->out, *lens = iovs->lens;
+    const uint64_t *first = chain_first;
+    uint32_t *dout = out;
+    if (dev) {
+        rc = enqueue_device(*d, *iovs, flags, st);
+        if (rc) return rc;
+    } else {  // stage the fold's inputs (small: 4-8 B per iov / chain)
+        const uint64_t n = iovs->n;
+        uint8_t *buf = (uint8_t *)d->grow(kScrStage, n * 8 + (nchains + 1) * 8 + nchains * 4 + 64);
+        if (!buf) return CRC32C_ENOMEM;
+        uint32_t *c_d = (uint32_t *)buf, *l_d = lens ? c_d + n : nullptr;
+        uint64_t *f_d = (uint64_t *)(buf + ((n * 8 + 7) & ~7ull));
+        uint32_t *o_d = (uint32_t *)(f_d + nchains + 1);
+        HIP_OK(hipMemcpyAsync(c_d, iovs->out, n * 4, hipMemcpyHostToDevice, st));
+        if (lens) HIP_OK(hipMemcpyAsync(l_d, lens, n * 4, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(f_d, chain_first, (nchains + 1) * 8, hipMemcpyHostToDevice, st));
+        crcs = c_d;
+        lens = l_d;
+        first = f_d;
+        dout = o_d;
+    }
+    const int g = (int)std::min<uint64_t>((nchains + 255) / 256, 4096);
+    hipLaunchKernelGGL(mcrc_dev::k_chain, dim3(g), dim3(256), 0, st, crcs, lens, iovs->len, first, nchains, dout,
+                       (const uint32_t *)d->xpow);
+    HIP_OK(hipGetLastError());
+    if (!dev) HIP_OK(hipMemcpyAsync(out, dout, nchains * 4, hipMemcpyDeviceToHost, st));
+    if (!dev || !(flags & CRC32C_ASYNC)) HIP_OK(hipStreamSynchronize(st));
     return CRC32C_OK;
 }
 
@@ -621,6 +699,12 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     hipStream_t st = (hipStream_t)stream;
     const bool dev = flags & CRC32C_DEVICE;
     const uint64_t nw = (base_bytes + wbuf_bytes - 1) / wbuf_bytes;
+    d->acquire(st);
+    struct Release {
+        Device *d;
+        hipStream_t st;
+        ~Release() { d->release(st); }
+    } release_on_exit{d, st};
     if (nw == 0 || nw >= 0x7fffffffull) {
         *nitems = *nbad = 0;
         return nw ? CRC32C_EINVAL : CRC32C_OK;

@@ -270,6 +270,38 @@ def test_verify_pages_device_walk(torch):
     assert nbad == len(bad_offs)
 
 
+def test_chained_iovs(torch):
+    """Chunked items (storage.c:163-170): the CRC chained over an item's iovs
+    (header from +32, then each chunk) equals crc32c(0, concatenation)."""
+    rng = np.random.default_rng(39)
+    buf = rng.integers(0, 256, 6 << 20, dtype=np.uint8)
+    nch = 120
+    counts = rng.integers(1, 12, nch)
+    counts[:3] = [1, 2, 40]
+    n = int(counts.sum())
+    lens = rng.integers(0, 600000, n).astype(np.uint32)
+    lens[:5] = [0, 3, 17, 524288, 1]
+    offs = rng.integers(0, buf.size - 600000, n).astype(np.uint64)
+    first = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    want = np.empty(nch, np.uint32)
+    for c in range(nch):
+        parts = [buf[int(o):int(o) + int(l)] for o, l in zip(offs[first[c]:first[c + 1]], lens[first[c]:first[c + 1]])]
+        cat = np.concatenate(parts) if parts else np.empty(0, np.uint8)
+        want[c] = oracle.batch(cat, np.zeros(1, np.uint64), np.array([cat.size]))[0]
+    got = mc.batch_chains(_dev(torch, buf), _dev(torch, offs.view(np.int64)), _dev(torch, lens.view(np.int32)),
+                          _dev(torch, first.view(np.int64)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(got), want)
+    # host path (iov offsets must be non-decreasing): the same chains over sorted iovs
+    offs_s = np.sort(offs)
+    want_s = np.empty(nch, np.uint32)
+    for c in range(nch):
+        sl = slice(int(first[c]), int(first[c + 1]))
+        cat = np.concatenate([buf[int(o):int(o) + int(l)] for o, l in zip(offs_s[sl], lens[sl])])
+        want_s[c] = oracle.batch(cat, np.zeros(1, np.uint64), np.array([cat.size]))[0]
+    np.testing.assert_array_equal(mc.batch_chains(buf, offs_s, lens, first), want_s)
+
+
 def test_realistic_item_spans_4133(torch):
     """config-1/config-5 geometry: 4133-byte spans at +32 of 4165-byte images."""
     items = [layout.make_item(b"key%07d" % i, np.random.default_rng(i).integers(0, 256, 4096, dtype=np.uint8).tobytes(),
