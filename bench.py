@@ -272,7 +272,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--items", type=int, default=ITEMS_PER_GPU, help="items per GPU (default: config 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="config2", choices=["config2", "config3", "config5", "host"],
+    ap.add_argument("--workload", default="config2",
+                    choices=["config2", "config2r", "config3", "config5", "pages", "stamp", "host"],
                     help="config2 = headline; others are extra measurements (not the bench line)")
     ap.add_argument("--pages", type=int, default=1000, help="config5: 64 MiB pages per GPU")
     args = ap.parse_args()
@@ -365,6 +366,53 @@ def extra_workload(args):
         res.update(config=cfg, kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
                    hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), nbad=nbad,
                    detected_exactly_the_injected_items=exact)
+    elif args.workload == "config2r":
+        # SURVEY.md 8(d) config 2 variant: realistic 4133-B spans at stride 4165, start +32 (unaligned)
+        n = args.items
+        g = torch.Generator(device="cuda").manual_seed(42 + rank)
+        data = torch.randint(0, 256, (n * 4165 + 64,), dtype=torch.uint8, device="cuda", generator=g)
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        spans = _lib.Spans(data.data_ptr() + 32, data.numel() - 32, None, 4165, None, 4133, None, out.data_ptr(), n)
+        run_steps(spans, max(1, args.warmup), stream)
+        torch.cuda.synchronize()
+        elapsed, evs = timed(lambda k: run_steps(spans, k, stream), args.steps, world)
+        kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        nbytes = n * 4133
+        res.update(config={"workload": f"config 2 variant: {n} x 4133-B spans at stride 4165, start +32 "
+                                       "(K2, one unit per span)"},
+                   kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
+                   hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+    elif args.workload in ("pages", "stamp"):
+        vargs, ok, victims, nbytes, cfg = workload_config5(args, rank, world)
+        base, size, region, offs, n, okp = vargs
+        nitems, nbad = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        sptr = ctypes.c_void_p(stream.cuda_stream)
+
+        def one():
+            if args.workload == "pages":  # device walk + verify (storage.c:950-1070)
+                _lib.check(_lib.lib.crc32c_verify_pages(base, size, region, None, None, 0, ctypes.byref(nitems),
+                                                        ctypes.byref(nbad), _lib.CRC32C_DEVICE, sptr))
+            else:  # spill CRCs stamped into every image (storage.c:567 per wbuf)
+                _lib.check(_lib.lib.crc32c_stamp_items(base, size, region, offs, n, None, ctypes.byref(nbad),
+                                                       _lib.CRC32C_DEVICE, sptr))
+
+        def steps(k):
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k)]
+            for a, b in evs:
+                a.record(stream)
+                one()
+                b.record(stream)
+            return evs
+
+        steps(max(1, args.warmup))
+        torch.cuda.synchronize()
+        elapsed, evs = timed(steps, args.steps, world)
+        kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        cfg["workload"] += (" -- walked on the device (crc32c_verify_pages)" if args.workload == "pages"
+                            else " -- stamped (crc32c_stamp_items)")
+        res.update(config=cfg, kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
+                   hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), nbad=int(nbad.value),
+                   nitems=int(nitems.value) if args.workload == "pages" else n, items_written=n)
     else:  # host: pinned host memory -> H2D -> K1/K2 -> D2H through the library's host path
         import numpy as np
         n = args.items

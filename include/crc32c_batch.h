@@ -19,6 +19,8 @@
  *                          (walk of storage.c:950-960): CRC over
  *                          [off + 32, off + ITEM_ntotal) against the value
  *                          stored in the item's exptime field (byte 28).
+ *   crc32c_host_alloc      pinned buffers for wbufs / readback_buf (SURVEY.md 8f
+ *                          rank 3).
  *   crc32c_batch_multi     crc32c_batch for host-resident batches split across
  *                          several GPUs by bytes (no collective: items are
  *                          independent).
@@ -128,6 +130,14 @@ int crc32c_stamp_items(void *base, uint64_t base_bytes, uint64_t region_bytes,
 typedef struct crc32c_job *crc32c_job_t;
 int crc32c_batch_submit(const crc32c_spans *spans, unsigned flags, crc32c_job_t *job);
 int crc32c_batch_wait(crc32c_job_t job);
+
+/* Page-locked host memory for extstore's wbufs (extstore.c:127-140) and the
+ * compaction readback_buf (storage.c:1120): host batches over such buffers
+ * are copied by one DMA per pipeline slot with no staging copy.  NULL when
+ * there is no gfx950 device or the allocation fails; free with
+ * crc32c_host_free. */
+void *crc32c_host_alloc(size_t bytes);
+void crc32c_host_free(void *p);
 
 const char *crc32c_strerror(int err);
 

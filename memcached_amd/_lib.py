@@ -28,7 +28,7 @@ CRC32C_ALIGNED16 = 0x4
 EXPORTED = (
     "crc32c", "crc32c_init", "crc32c_sw", "crc32c_sw_little",
     "crc32c_gpu_count", "crc32c_batch", "crc32c_batch_multi", "crc32c_verify_items", "crc32c_stamp_items",
-    "crc32c_verify_pages", "crc32c_batch_chains",
+    "crc32c_verify_pages", "crc32c_batch_chains", "crc32c_host_alloc", "crc32c_host_free",
     "crc32c_batch_submit", "crc32c_batch_wait", "crc32c_strerror", "crc32c_last_kernel_ms",
 )
 
@@ -86,6 +86,10 @@ def _load():
     lib.crc32c_batch_chains.restype = ctypes.c_int
     lib.crc32c_batch_chains.argtypes = [ctypes.POINTER(Spans), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_uint, ctypes.c_void_p]
+    lib.crc32c_host_alloc.restype = ctypes.c_void_p
+    lib.crc32c_host_alloc.argtypes = [ctypes.c_size_t]
+    lib.crc32c_host_free.restype = None
+    lib.crc32c_host_free.argtypes = [ctypes.c_void_p]
     lib.crc32c_batch_submit.restype = ctypes.c_int
     lib.crc32c_batch_submit.argtypes = [ctypes.POINTER(Spans), ctypes.c_uint, ctypes.POINTER(ctypes.c_void_p)]
     lib.crc32c_batch_wait.restype = ctypes.c_int

@@ -589,6 +589,18 @@ int crc32c_gpu_count(void) {
     return g_ndev;
 }
 
+void *crc32c_host_alloc(size_t bytes) {
+    if (bytes == 0 || crc32c_gpu_count() <= 0) return nullptr;
+    void *p = nullptr;
+    // portable: usable by every device's copy engine (crc32c_batch_multi)
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) return nullptr;
+    return p;
+}
+
+void crc32c_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
 const char *crc32c_strerror(int err) {
     switch (err) {
         case CRC32C_OK: return "ok";

@@ -91,7 +91,17 @@ int main(int argc, char **argv) {
     CHECK(crc32c(0, "123456789", 9) == 0xe3069283u, "check value");
 
     /* ---- write path: pack images into wbufs (extstore.c:627-659) ---- */
-    uint8_t *ref = calloc(NWBUF, WBUF), *bat = calloc(NWBUF, WBUF);
+    /* the batched wbufs are pinned (extstore.c:127-140 with crc32c_host_alloc):
+     * the host path then DMAs them without a staging copy */
+    uint8_t *ref = calloc(NWBUF, WBUF), *bat = gpu ? crc32c_host_alloc((size_t)NWBUF * WBUF) : NULL;
+    if (!gpu) {
+        CHECK(crc32c_host_alloc(4096) == NULL, "pinned allocation without a GPU must fail");
+        bat = calloc(NWBUF, WBUF);
+    }
+    if (!ref || !bat) {
+        fprintf(stderr, "allocation failed\n");
+        return 2;
+    }
     uint64_t *offs = malloc(sizeof(uint64_t) * NWBUF * WBUF / 64);
     uint64_t n = 0;
     for (uint32_t w = 0; w < NWBUF; ++w) {
@@ -163,5 +173,6 @@ int main(int argc, char **argv) {
     }
     printf("storage_sim: %llu items stamped and verified, %u reads, badcrc %u\n", (unsigned long long)n, nrd,
            badcrc);
+    crc32c_host_free(bat);
     return fails ? 1 : 0;
 }

@@ -302,6 +302,23 @@ def test_chained_iovs(torch):
     np.testing.assert_array_equal(mc.batch_chains(buf, offs_s, lens, first), want_s)
 
 
+def test_pinned_host_alloc():
+    """crc32c_host_alloc buffers (pinned wbufs) take the host path with no
+    staging copy and give the same CRCs."""
+    import ctypes
+    nbytes = 3 << 20
+    p = _lib.lib.crc32c_host_alloc(nbytes)
+    assert p
+    try:
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
+        arr[:] = np.random.default_rng(40).integers(0, 256, nbytes, dtype=np.uint8)
+        offs = np.arange(0, nbytes - 5000, 4165, dtype=np.uint64) + 32
+        lens = np.full(offs.size, 4133, np.uint32)
+        np.testing.assert_array_equal(mc.batch(arr, offsets=offs, lens=lens), oracle.batch(arr, offs, lens))
+    finally:
+        _lib.lib.crc32c_host_free(p)
+
+
 def test_realistic_item_spans_4133(torch):
     """config-1/config-5 geometry: 4133-byte spans at +32 of 4165-byte images."""
     items = [layout.make_item(b"key%07d" % i, np.random.default_rng(i).integers(0, 256, 4096, dtype=np.uint8).tobytes(),
