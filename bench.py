@@ -141,11 +141,19 @@ def cpu_baseline(data: torch.Tensor, out: torch.Tensor):
 
     one = rate(1, 5)
     many = rate(cores, 20)
+    model = "unknown CPU"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     gpu = out[:n].cpu().numpy().view(np.uint32)
     return {"value": round(many, 2), "unit": "GiB/s", "cores": cores, "kind": "reference",
             "sample": f"first 65536 x 4096 B items of the GPU batch (256 MiB), reference crc32c.c "
                       f"(hw dispatch) per item as storage.c:567, {cores} threads static split, best of 20; "
-                      f"1 core: {one:.2f} GiB/s",
+                      f"1 core: {one:.2f} GiB/s; {model}",
             "gpu_match": bool((gpu == crc).all())}
 
 
@@ -331,7 +339,7 @@ def main():
             "kernel_ms": round(kernel_ms, 4),
         },
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU leg runs at N = 1 only
         result["cpu_baseline"] = cpu_baseline(data, out)
     if rank == 0:
         print(json.dumps(result), flush=True)

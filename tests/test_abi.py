@@ -66,3 +66,35 @@ def test_errors_are_named():
 
 def test_batch_rejects_null_descriptor():
     assert _lib.lib.crc32c_batch(None, 0, None) == _lib.CRC32C_EINVAL
+
+
+def test_no_gpu_means_enodev_not_a_cpu_fallback():
+    """Every batch entry point fails loudly without a gfx950 device (CPU leg
+    only: skipped where a GPU is visible)."""
+    if _lib.lib.crc32c_gpu_count() > 0:
+        pytest.skip("a gfx950 device is visible")
+    buf = np.zeros(1 << 16, np.uint8)
+    offs = np.zeros(4, np.uint64)
+    lens = np.full(4, 100, np.uint32)
+    out = np.zeros(4, np.uint32)
+    s = _lib.Spans(buf.ctypes.data, buf.size, offs.ctypes.data, 0, lens.ctypes.data, 0, None, out.ctypes.data, 4)
+    nbad, nitems = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    ok = np.zeros(4, np.uint8)
+    first = np.array([0, 2, 4], np.uint64)
+    calls = {
+        "crc32c_batch": lambda: _lib.lib.crc32c_batch(ctypes.byref(s), 0, None),
+        "crc32c_batch_multi": lambda: _lib.lib.crc32c_batch_multi(ctypes.byref(s), 1),
+        "crc32c_verify_items": lambda: _lib.lib.crc32c_verify_items(buf.ctypes.data, buf.size, 0, offs.ctypes.data,
+                                                                    4, ok.ctypes.data, ctypes.byref(nbad), 0, None),
+        "crc32c_stamp_items": lambda: _lib.lib.crc32c_stamp_items(buf.ctypes.data, buf.size, 0, offs.ctypes.data,
+                                                                  4, ok.ctypes.data, ctypes.byref(nbad), 0, None),
+        "crc32c_verify_pages": lambda: _lib.lib.crc32c_verify_pages(buf.ctypes.data, buf.size, 1 << 12, None, None,
+                                                                    0, ctypes.byref(nitems), ctypes.byref(nbad),
+                                                                    0, None),
+        "crc32c_batch_chains": lambda: _lib.lib.crc32c_batch_chains(ctypes.byref(s), first.ctypes.data, 2,
+                                                                    out.ctypes.data, 0, None),
+    }
+    for name, call in calls.items():
+        assert call() == _lib.CRC32C_ENODEV, name
+    assert _lib.lib.crc32c_host_alloc(4096) is None
+    assert (out == 0).all()  # nothing was computed on the CPU

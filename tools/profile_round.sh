@@ -1,6 +1,7 @@
 #!/bin/bash
-# Evidence for one round: GPU tests, smoke, bench, rocprofv3 summaries.
-#   bash tools/profile_round.sh r01
+# Evidence for one round: GPU tests, smoke, bench, rocprofv3 summaries of the
+# headline and of the span workloads, HBM traffic, extra workload lines.
+#   bash tools/profile_round.sh r01        (then: bash tools/collect_profiles.sh r01)
 source tools/gpu_guard.sh
 export TMPDIR=/tmp
 R=${1:-r01}
@@ -8,8 +9,11 @@ O=gpurun_out/$R; mkdir -p $O
 run 900 python -m pytest tests -x -q -m gpu > $O/pytest_gpu.log 2>&1
 run 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 run 600 python bench.py > $O/bench.json 2> $O/bench.err
-run 600 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python bench.py --no-cpu-baseline > $O/kt_bench.json 2> $O/kt.err
-run 600 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o fetch --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/fetch.log 2>&1
-run 600 rocprofv3 --pmc WRITE_SIZE -d $O/write -o write --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/write.log 2>&1
+run 600 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 bench.py --no-cpu-baseline > $O/kt_bench.json 2> $O/kt.err
+run 600 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o fetch --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/fetch.log 2>&1
+run 600 rocprofv3 --pmc WRITE_SIZE -d $O/write -o write --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/write.log 2>&1
 run 60 python tools/traffic.py $O/fetch $O/write $O/traffic.json > /dev/null
+run 600 rocprofv3 --kernel-trace --stats -d $O/kt_c3 -o c3 --output-format csv -- python3 bench.py --workload config3 --steps 3 --warmup 1 > $O/kt_c3.json 2> $O/kt_c3.err
+run 600 rocprofv3 --kernel-trace --stats -d $O/kt_c5 -o c5 --output-format csv -- python3 bench.py --workload config5 --pages 300 --steps 3 --warmup 1 > $O/kt_c5.json 2> $O/kt_c5.err
+mkdir -p $O/x && bash tools/extra_workloads.sh $R/x
 echo done
