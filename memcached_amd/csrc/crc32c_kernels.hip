@@ -432,18 +432,16 @@ __device__ __forceinline__ uint32_t fetch_unit(const SpanArgs &a, uint64_t u, ui
     if (u >= nunits) return 0u;  // flags 0: no unit
     if (UNITS) return reinterpret_cast<const uint32_t *>(a.units + u)[j];
     // MODE 0, one unit per span: raw item fields {off lo, off hi, len, -, crc_in, u, 1, -}
-    switch (j) {
-        case 0:
-        case 1: {
-            const uint64_t off = a.offsets ? a.offsets[u] : u * a.stride;
-            return (uint32_t)(off >> (32 * j));
-        }
-        case 2: return a.lens ? a.lens[u] : a.len;
-        case 4: return a.crc_in ? a.crc_in[u] : 0u;
-        case 5: return (uint32_t)u;
-        case 6: return 1u;
-        default: return 0u;
-    }
+    // (selected without branching on the lane: every lane reads the same words)
+    const uint64_t off = a.offsets ? a.offsets[u] : u * a.stride;
+    const uint32_t len = a.lens ? a.lens[u] : a.len;
+    const uint32_t cin = a.crc_in ? a.crc_in[u] : 0u;
+    uint32_t v = j == 0 ? (uint32_t)off : (uint32_t)(off >> 32);
+    v = j == 2 ? len : v;
+    v = j == 4 ? cin : v;
+    v = j == 5 ? (uint32_t)u : v;
+    v = j == 6 ? 1u : v;
+    return (j == 3 || j == 7) ? 0u : v;
 }
 
 template <int MODE, bool UNITS>
@@ -473,15 +471,21 @@ struct BlockWin {
 // Issue the loads of block k of unit d for lane li.
 __device__ __forceinline__ void load_block(BlockWin &w, const UnitDesc &d, uint32_t k, uint32_t li,
                                            const uint4 *zero) {
-    const uint8_t *G = d.e() - (size_t)kBlockBytes * (d.niters - k);
-    const uint8_t *E = d.E();
+    // offsets relative to the unit's first byte p: block start G - p = grel;
+    // piece rel = grel + 1024 r + 32 li + 16 j overlaps [p, E) iff
+    // -16 < rel < Eo, i.e. (uint32)(rel + 15) < Eo + 15.  (A unit with no
+    // bytes has Eo == 0 and reads only zeros.)
+    const int32_t grel = (int32_t)d.eo - (int32_t)(kBlockBytes * (d.niters - k));
+    const int32_t lrel = grel + (int32_t)(kSpanCH * li);
+    const uint8_t *q0 = d.p + lrel;
+    const uint32_t lim = d.Eo + 15u;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const uint8_t *q = G + r * kRowBytes + kSpanCH * li + 16 * j;
-            const bool ok = q + 16 > d.p && q < E;  // (an invalid unit has E == p)
-            w.v[r][j] = ld16(ok ? reinterpret_cast<const uint4 *>(q) : zero);
+            const int32_t off = r * (int32_t)kRowBytes + 16 * j;
+            const bool ok = (uint32_t)(lrel + off + 15) < lim;
+            w.v[r][j] = ld16(ok ? reinterpret_cast<const uint4 *>(q0 + off) : zero);
         }
 }
 
@@ -651,24 +655,22 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         }
 
         if (cur.niters) {
-            const uint8_t *G = cur.e() - (size_t)kBlockBytes * (cur.niters - k);
-            const uint8_t *q0 = G + kSpanCH * li;  // this lane's piece 0 of row 0
+            const int32_t grel = (int32_t)cur.eo - (int32_t)(kBlockBytes * (cur.niters - k));  // G - p
             // head: zero the bytes before p and inject ~crc_in into [p, p+4).
             // Only the lane owning the piece ph that holds p is touched (and,
             // when p & 15 > 12, dword 0 of the next piece, which is in block 1
             // when ph ends block 0).  The owner and the piece follow from
             // rel = ph - q0: lane li owns it iff 0 <= rel < 4096 and
             // rel % 1024 < 32; then it is piece (rel >> 10, (rel >> 4) & 1).
-            const uint8_t *ph = (const uint8_t *)((uintptr_t)cur.p & ~(uintptr_t)15);
             const uint32_t kh = (uint32_t)((uintptr_t)cur.p & 15u);
 #ifdef MCRC_ABL_NOHEAD  // ablation: skip head masking and ~crc_in injection (wrong CRCs)
             const bool hd = false, hd2 = false;
 #else
             const bool hd = k == 0 && cur.head();
-            const bool hd2 = cur.head() && kh > 12 && cur.Eo >= 4 && (k == 0 || (k == 1 && ph + 16 == G));
+            const bool hd2 = cur.head() && kh > 12 && cur.Eo >= 4 && (k == 0 || (k == 1 && 16 - (int32_t)kh == grel));
 #endif
             if (__any(hd || hd2)) {
-                const int32_t rel = (int32_t)(ph - q0), rel2 = rel + 16;
+                const int32_t rel = -(int32_t)kh - grel - (int32_t)(kSpanCH * li), rel2 = rel + 16;  // ph - q0
                 const auto piece_of = [](int32_t x, bool en) -> int32_t {
                     return en && x >= 0 && x < (int32_t)kBlockBytes && (x & (kRowBytes - 1)) < (int32_t)kSpanCH
                                ? 2 * (x >> 10) + ((x >> 4) & 1)
@@ -708,10 +710,10 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
             }
             // rows wholly before p for every lane of the wave are skipped
             // (a group without a unit has niters == 0 and votes to skip)
-            const uint32_t nskip = __all(G + 3 * kRowBytes <= cur.p)   ? 3u
-                                   : __all(G + 2 * kRowBytes <= cur.p) ? 2u
-                                   : __all(G + kRowBytes <= cur.p)     ? 1u
-                                                                       : 0u;
+            const uint32_t nskip = __all(grel + 3 * (int32_t)kRowBytes <= 0)   ? 3u
+                                   : __all(grel + 2 * (int32_t)kRowBytes <= 0) ? 2u
+                                   : __all(grel + (int32_t)kRowBytes <= 0)     ? 1u
+                                                                               : 0u;
             uint32_t v;
             switch (nskip) {
                 case 0: v = block_value<0>(w, c); break;
@@ -866,10 +868,11 @@ __global__ void k_walk(const uint8_t *base, uint64_t bytes, uint64_t wbuf, uint6
         const uint64_t o0 = prefix ? prefix[w] : 0;
         while (off + 48 <= size) {
             const uint8_t *it = base + start + off;
+            // every header field is read before the nkey test: one round trip per item
             const uint32_t nkey = it[41];
-            if (nkey == 0) break;  // zeroed tail of the wbuf
             const uint32_t nbytes = ld_u32_unaligned(it + 32);
             const uint32_t flags = it[38] | (it[39] << 8);
+            if (nkey == 0) break;  // zeroed tail of the wbuf
             if (prefix) offs[o0 + c] = start + off;
             ++c;
             off += 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) + ((flags & 2u) ? 8 : 0);
