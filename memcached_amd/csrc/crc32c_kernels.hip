@@ -699,7 +699,11 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
             }
             // tail: zero the bytes >= E in the span's last piece
             const uint32_t te = cur.eo - cur.Eo;
+#ifdef MCRC_ABL_NOTAIL  // ablation: no tail masking (wrong CRCs)
+            const bool ht = false;
+#else
             const bool ht = last && li == 31 && te - 1u < 15u;
+#endif
             if (__any(ht)) {
                 const uint32_t kt = 16u - te;
                 uint4 &v = w.v[3][1];
@@ -731,7 +735,11 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
                     const uint32_t aux = __shfl(cur.raw, (lane & 32u) | 4u, 64);
                     const uint32_t item = __shfl(cur.raw, (lane & 32u) | 5u, 64);
                     if (li == 0 && cur.Eo < 4) raw ^= short_init<MODE>(a, aux, cur.Eo, t);
+#ifdef MCRC_ABL_NOFIN  // ablation: no x^-8t multiply (wrong CRCs)
+                    const uint32_t v = raw ^ t;
+#else
                     const uint32_t v = mul_xinv_group(raw, t, li);
+#endif
                     if (li == 0) emit<MODE>(a, item, ~v, aux, cur.sane(), cur.p);
                 } else {
                     // segment s of nseg: raw_v(span) gets M_{64Ki * (nseg-1-s)}(raw)
@@ -856,16 +864,22 @@ __global__ void k_chain(const uint32_t *iov_crc, const uint32_t *lens, uint32_t 
 // buffer is a sequence of wbuf-sized reads; in each, items are packed from
 // offset 0, nkey == 0 ends the wbuf, the next item is at + ITEM_ntotal, and the
 // walk stops when fewer than sizeof(item) = 48 bytes remain.  One thread per
-// wbuf (the walk is a dependent chain).  Pass 1 (prefix == nullptr) counts the
-// items of every wbuf; pass 2 writes their offsets at prefix[w].
+// wbuf (the walk is a dependent chain, one header round trip per item).
+//   k_walk (slots != nullptr): count the items of wbuf w into cnt[w] and keep
+//     the first kWalkSlots offsets (relative to the wbuf) in slots[w][];
+//   k_walk_place: copy the kept offsets to offs[prefix[w] + i];
+//   k_walk (slots == nullptr, prefix != nullptr): re-walk only the wbufs that
+//     held more than kWalkSlots items, writing offsets >= kWalkSlots.
+constexpr uint32_t kWalkSlots = 2048;
+
 __global__ void k_walk(const uint8_t *base, uint64_t bytes, uint64_t wbuf, uint64_t nw, uint32_t *cnt,
-                       const uint32_t *prefix, uint64_t *offs) {
+                       uint32_t *slots, const uint32_t *prefix, uint64_t *offs) {
     for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nw;
          w += (uint64_t)gridDim.x * blockDim.x) {
+        if (!slots && cnt[w] <= kWalkSlots) continue;  // second pass: overflowed wbufs only
         const uint64_t start = w * wbuf, size = bytes - start < wbuf ? bytes - start : wbuf;
         uint64_t off = 0;
         uint32_t c = 0;
-        const uint64_t o0 = prefix ? prefix[w] : 0;
         while (off + 48 <= size) {
             const uint8_t *it = base + start + off;
             // every header field is read before the nkey test: one round trip per item
@@ -873,11 +887,24 @@ __global__ void k_walk(const uint8_t *base, uint64_t bytes, uint64_t wbuf, uint6
             const uint32_t nbytes = ld_u32_unaligned(it + 32);
             const uint32_t flags = it[38] | (it[39] << 8);
             if (nkey == 0) break;  // zeroed tail of the wbuf
-            if (prefix) offs[o0 + c] = start + off;
+            if (slots) {
+                if (c < kWalkSlots) slots[w * kWalkSlots + c] = (uint32_t)off;
+            } else if (c >= kWalkSlots) {
+                offs[prefix[w] + c] = start + off;
+            }
             ++c;
             off += 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) + ((flags & 2u) ? 8 : 0);
         }
-        if (!prefix) cnt[w] = c;
+        if (slots) cnt[w] = c;
+    }
+}
+
+__global__ void k_walk_place(uint64_t wbuf, uint64_t nw, const uint32_t *cnt, const uint32_t *slots,
+                             const uint32_t *prefix, uint64_t *offs) {
+    for (uint64_t w = blockIdx.x; w < nw; w += gridDim.x) {
+        const uint32_t c = cnt[w] < kWalkSlots ? cnt[w] : kWalkSlots;
+        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x)
+            offs[prefix[w] + i] = w * wbuf + slots[w * kWalkSlots + i];
     }
 }
 

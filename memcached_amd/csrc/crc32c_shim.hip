@@ -106,7 +106,7 @@ struct Device {
     struct Scratch {
         void *p = nullptr;
         size_t bytes = 0;
-    } scratch[7];
+    } scratch[8];
     void *grow(int slot, size_t bytes) {
         Scratch &s = scratch[slot];
         if (s.bytes < bytes) {
@@ -119,7 +119,7 @@ struct Device {
         return s.p;
     }
 };
-enum { kScrWalkCnt, kScrWalkCnt1, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage };
+enum { kScrWalkCnt, kScrWalkCnt1, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage, kScrWalkSlots };
 
 std::mutex g_dev_mu;
 std::vector<std::unique_ptr<Device>> g_devs;
@@ -735,7 +735,9 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     void *scan = d->grow(kScrWalkScan, tmp);
     if (!cnt || !prefix || !scan) return CRC32C_ENOMEM;
     const int gw = (int)std::min<uint64_t>((nw + 255) / 256, 1024);
-    hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(256), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt,
+    uint32_t *slots = (uint32_t *)d->grow(kScrWalkSlots, nw * mcrc_dev::kWalkSlots * 4);
+    if (!slots) return CRC32C_ENOMEM;
+    hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(256), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt, slots,
                        (const uint32_t *)nullptr, (uint64_t *)nullptr);
     // prefix[nw] = total: scan nw + 1 counts with a zero appended
     uint32_t *cnt1 = (uint32_t *)d->grow(kScrWalkCnt1, (nw + 1) * 4);
@@ -755,8 +757,10 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     uint64_t *doffs = direct ? offsets : (uint64_t *)d->grow(kScrWalkOffs, (size_t)total * 8);
     uint8_t *dok = direct ? ok : (uint8_t *)d->grow(kScrWalkOk, total);
     if (!doffs || !dok) return CRC32C_ENOMEM;
+    hipLaunchKernelGGL(mcrc_dev::k_walk_place, dim3((int)std::min<uint64_t>(nw, 8192)), dim3(256), 0, st, wbuf_bytes,
+                       nw, (const uint32_t *)cnt, (const uint32_t *)slots, (const uint32_t *)prefix, doffs);
     hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(256), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt,
-                       (const uint32_t *)prefix, doffs);
+                       (uint32_t *)nullptr, (const uint32_t *)prefix, doffs);
     mcrc_dev::SpanArgs a{};
     a.base = dbase;
     a.base_bytes = base_bytes;

@@ -319,6 +319,23 @@ def test_pinned_host_alloc():
         _lib.lib.crc32c_host_free(p)
 
 
+def test_verify_pages_many_small_items(torch):
+    """More items per wbuf than the walk keeps per pass (2048): the overflow
+    re-walk places the rest."""
+    rng = np.random.default_rng(41)
+    items = [layout.make_item(b"s%05d" % i, rng.integers(0, 256, int(rng.integers(0, 24)), dtype=np.uint8).tobytes(),
+                              cas=i + 1) for i in range(9000)]
+    wbuf = 256 << 10
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    assert np.bincount((offs // wbuf).astype(np.int64)).max() > 2048
+    ok, nbad = mc.stamp_items(buf, offs, region_bytes=wbuf)
+    assert nbad == 0
+    buf[int(offs[5000]) + 40] ^= 1  # nkey byte is 41: flip a header byte inside the span instead
+    got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, buf), wbuf)
+    np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), offs)
+    assert nbad == 1 and got_ok.cpu().numpy()[5000] == 0
+
+
 def test_realistic_item_spans_4133(torch):
     """config-1/config-5 geometry: 4133-byte spans at +32 of 4165-byte images."""
     items = [layout.make_item(b"key%07d" % i, np.random.default_rng(i).integers(0, 256, 4096, dtype=np.uint8).tobytes(),
