@@ -219,6 +219,19 @@ def test_stamp_items(torch):
                                            ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     torch.cuda.synchronize()
     np.testing.assert_array_equal(d.cpu().numpy(), want)
+    # long images (> 64 KiB: several work units, stamped by the combine pass)
+    big = [layout.make_item(b"lg%05d" % i, rng.integers(0, 256, int(rng.integers(65000, 400000)),
+                                                        dtype=np.uint8).tobytes(), cas=i + 1) for i in range(30)]
+    bbuf, boffs = layout.pack_wbufs(big, 1 << 20)
+    bso, bsl = layout.spans_of(bbuf, boffs)
+    bwant = bbuf.copy()
+    layout.store_crcs(bwant, boffs, oracle.batch(bbuf, bso, bsl))
+    bd = _dev(torch, bbuf)
+    ok, nbad = mc.stamp_items(bd, _dev(torch, boffs.view(np.int64)), region_bytes=1 << 20)
+    assert nbad == 0
+    np.testing.assert_array_equal(bd.cpu().numpy(), bwant)
+    ok, nbad = mc.stamp_items(bbuf, boffs, region_bytes=1 << 20)
+    np.testing.assert_array_equal(bbuf, bwant)
     # malformed: nbytes claims a span past the wbuf -> not stamped, counted
     bad = buf.copy()
     bad[int(offs[11]) + 32 + 2] ^= 0x10
