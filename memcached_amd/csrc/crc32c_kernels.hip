@@ -19,6 +19,10 @@
 
 namespace mcrc_dev {
 
+#ifdef MCRC_UBENCH_CLOCK  // dev tool (tools/ubench.hip): per-block core clock vs wall clock
+__device__ uint64_t *g_clock_stamps;
+#endif
+
 // ===========================================================================
 // K1: fixed-length aligned items
 // ===========================================================================
@@ -36,6 +40,7 @@ template <int LPI, int CH, int R>
 struct ItemRegs {
     static constexpr int Q = CH / 16;
     uint4 d[R][Q];
+    uint32_t cin;  // MODE 11: the item's initial CRC
 
     __device__ __forceinline__ void load(const uint8_t *__restrict__ p, uint32_t li) {
 #pragma unroll
@@ -43,6 +48,13 @@ struct ItemRegs {
 #pragma unroll
             for (int q = 0; q < Q; ++q)
                 d[r][q] = ld16(p + (size_t)r * LPI * CH + li * CH + 16 * q);
+    }
+    // wb: wave-uniform base (SGPR), loff: this lane's byte offset from it
+    __device__ __forceinline__ void load_at(const uint8_t *__restrict__ wb, uint32_t loff) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < Q; ++q) d[r][q] = ld16(wb + loff + (r * LPI * CH + 16 * q));
     }
     __device__ __forceinline__ uint32_t checksum() const {
         uint32_t a = 0;
@@ -83,7 +95,7 @@ __device__ __forceinline__ uint32_t lane_partial(const ItemRegs<LPI, CH, R> &it,
 }
 
 // Lane partial for SLICE 4, LPI 32: chains fused with bitop3 XORs.
-template <int CH, int R>
+template <int CH, int R, bool FOLD = true>
 __device__ __forceinline__ uint32_t lane_partial_x3(const ItemRegs<32, CH, R> &it, const LaneCtx &c) {
     constexpr int Q = CH / 16;
     constexpr int N = 4 * Q;  // dwords per chain
@@ -100,7 +112,7 @@ __device__ __forceinline__ uint32_t lane_partial_x3(const ItemRegs<32, CH, R> &i
     }
     uint32_t a = x[0];
 #pragma unroll
-    for (int r = 1; r < R; ++r) a = apply_op<4>(kAuxOp5, a) ^ x[r];
+    for (int r = 1; r < R; ++r) a = (FOLD ? apply_op<4>(kAuxOp5, a) : a) ^ x[r];
     return a;
 }
 
@@ -153,7 +165,13 @@ __device__ __forceinline__ uint32_t lane_partial_x3_feed(const ItemRegs<32, CH, 
 // MODE 1: loads only; MODE 2: no lane-group reduction; MODE 3: data chains only.
 // MODE 4/5: full CRC, optimised variants (SLICE 4, LPI 32 only).
 // MODE 6: MODE 5 with the next step's loads spread over the chains.
-template <int SLICE, int LPI, int CH, int R, int MODE, int DEPTH = 2, int STAGGER = 0>
+// MODE 7: MODE 5 chains without row folds or lane reduction (ablation).
+// MODE 9/10: MODE 1 plus s_sleep 20/40 per step (ablation: compute-like gaps).
+// MODE 11: MODE 5 with ~crc_in injected into the first data dword (CRCIN:
+//          crc_in[] is loaded with the item; otherwise crc_in = 0).
+// PRIO > 0: the wave raises its issue priority while it issues loads.
+template <int SLICE, int LPI, int CH, int R, int MODE, int DEPTH = 2, int STAGGER = 0, int PRIO = 0,
+          bool SCHED_FENCE = false, bool CRCIN = false>
 __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base, uint64_t stride,
                                                 uint64_t nitems, const uint4 *__restrict__ img,
                                                 uint32_t kfinal, uint32_t kspan,
@@ -161,6 +179,9 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
                                                 uint32_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     load_tables(smem, img, LdsImage<SLICE>::bytes);
+#ifdef MCRC_UBENCH_CLOCK
+    const uint64_t clk0 = clock64(), wall0 = wall_clock64();
+#endif
     constexpr uint32_t IPW = 64 / LPI;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t li = lane % LPI;
@@ -171,7 +192,11 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     const uint64_t waves = blockDim.x >> 6;
     const uint64_t gstep = gridDim.x * waves;
     const uint64_t ngroups = (nitems + IPW - 1) / IPW;
-    uint64_t grp = blockIdx.x * waves + (threadIdx.x >> 6);
+    // wave-uniform (SGPR) group index: the loop exits are then scalar
+    // branches, and the waitcnt pass sees one path into the loop header (a
+    // divergent exit merged an un-waited path there and forced vmcnt(0),
+    // which drained the prefetched step).
+    uint64_t grp = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
     if (grp >= ngroups) return;
     if constexpr (STAGGER > 0) {
         // desynchronise the workgroup's waves: odd waves start STAGGER x 8K cycles late
@@ -183,14 +208,28 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     auto clamp = [&](uint64_t it) { return it < nitems ? it : nitems - 1; };
     auto finish = [&](const ItemRegs<LPI, CH, R> &regs, uint64_t gi) {
         const uint64_t item = item_of(gi);
-        if (MODE == 1) {
+        if (MODE == 1 || MODE == 9 || MODE == 10) {
             const uint32_t a = regs.checksum();
+            if (MODE == 9) __builtin_amdgcn_s_sleep(20);
+            if (MODE == 10) __builtin_amdgcn_s_sleep(40);
             if (a == 0x9e3779b9u && item < nitems) out[item] = a;
             return;
         }
         uint32_t raw;
+        if (MODE == 11) {
+            // ~crc_in injected into the item's first dword: a register seeded
+            // with ~crc_in adds exactly M_len(~crc_in) (crc32c.c:166), so
+            // crc32c(crc_in, D) = ~raw(D ^ (~crc_in || 0...)) -- no multiply.
+            ItemRegs<LPI, CH, R> &m = const_cast<ItemRegs<LPI, CH, R> &>(regs);
+            if (li == 0) m.d[0][0].x ^= ~m.cin;
+            raw = group_reduce32_dpp(lane_partial_x3<CH, R>(m, c), lane);
+            if (li == 0 && item < nitems) out[item] = ~raw;
+            return;
+        }
         if (MODE == 5)  // optimised: bitop3 chains + DPP reduction (SLICE 4, LPI 32)
             raw = group_reduce32_dpp(lane_partial_x3<CH, R>(regs, c), lane);
+        else if (MODE == 7)
+            raw = lane_partial_x3<CH, R, false>(regs, c);
         else if (MODE == 4)  // bitop3 chains, LDS-shuffle reduction
             raw = group_reduce<SLICE, LPI>(lane_partial_x3<CH, R>(regs, c), lane);
         else if (MODE == 3)
@@ -206,6 +245,27 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 
     auto addr = [&](uint64_t gi) { return base + clamp(item_of(gi < ngroups ? gi : ngroups - 1)) * stride; };
     ItemRegs<LPI, CH, R> ra, rb;
+    // The sched_barrier keeps the next step's loads at the top of the step:
+    // left alone, the scheduler sinks them into the chains (to shorten their
+    // live ranges), so the following step waits on loads issued moments before.
+    auto ld = [&](ItemRegs<LPI, CH, R> &r, uint64_t gi) {
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
+        if constexpr (MODE == 11) {
+            // uniform step base + per-lane offset: no 64-bit VGPR address math
+            // (and no fresh temporaries) at the top of a step
+            const uint64_t gu = gi < ngroups ? gi : ngroups - 1;
+            const uint64_t first = gu * IPW;
+            const uint8_t *wb = base + first * stride;
+            const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
+            r.load_at(wb, gl * (uint32_t)stride + li * CH);
+            if constexpr (CRCIN) r.cin = crc_in[first + gl];
+            else r.cin = 0u;
+        } else {
+            r.load(addr(gi), li);
+        }
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
+        if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
+    };
     if constexpr (MODE == 6) {
         // loads of the next step interleaved with this step's chains
         auto fin6 = [&](const ItemRegs<LPI, CH, R> &cur, ItemRegs<LPI, CH, R> &nxt, uint64_t gi) {
@@ -224,14 +284,29 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
             grp += gstep;
             if (grp >= ngroups) break;
         }
+    } else if (DEPTH == 2 && MODE == 11) {
+        // One exit, at the bottom: a break between the two halves would give
+        // the loop header a second (un-waited) predecessor, and the waitcnt
+        // pass would then drain every prefetched load there.
+        const uint64_t nsteps = (ngroups - grp + gstep - 1) / gstep;
+        ld(ra, grp);
+        for (uint64_t k = 0; k + 2 <= nsteps; k += 2) {
+            ld(rb, grp + gstep);
+            finish(ra, grp);
+            grp += gstep;
+            ld(ra, grp + gstep);
+            finish(rb, grp);
+            grp += gstep;
+        }
+        if (nsteps & 1) finish(ra, grp);
     } else if (DEPTH == 2) {
-        ra.load(addr(grp), li);
+        ld(ra, grp);
         for (;;) {
-            rb.load(addr(grp + gstep), li);
+            ld(rb, grp + gstep);
             finish(ra, grp);
             grp += gstep;
             if (grp >= ngroups) break;
-            ra.load(addr(grp + gstep), li);
+            ld(ra, grp + gstep);
             finish(rb, grp);
             grp += gstep;
             if (grp >= ngroups) break;
@@ -239,23 +314,32 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     } else {
         // three register buffers: two steps in flight while one is reduced
         ItemRegs<LPI, CH, R> rc;
-        ra.load(addr(grp), li);
-        rb.load(addr(grp + gstep), li);
+        ld(ra, grp);
+        ld(rb, grp + gstep);
         for (;;) {
-            rc.load(addr(grp + 2 * gstep), li);
+            ld(rc, grp + 2 * gstep);
             finish(ra, grp);
             grp += gstep;
             if (grp >= ngroups) break;
-            ra.load(addr(grp + 2 * gstep), li);
+            ld(ra, grp + 2 * gstep);
             finish(rb, grp);
             grp += gstep;
             if (grp >= ngroups) break;
-            rb.load(addr(grp + 2 * gstep), li);
+            ld(rb, grp + 2 * gstep);
             finish(rc, grp);
             grp += gstep;
             if (grp >= ngroups) break;
         }
     }
+#ifdef MCRC_UBENCH_CLOCK
+    if (threadIdx.x == 0) {
+        const uint64_t clk1 = clock64(), wall1 = wall_clock64();
+        g_clock_stamps[4 * blockIdx.x + 0] = clk0;
+        g_clock_stamps[4 * blockIdx.x + 1] = clk1;
+        g_clock_stamps[4 * blockIdx.x + 2] = wall0;
+        g_clock_stamps[4 * blockIdx.x + 3] = wall1;
+    }
+#endif
 }
 
 // ===========================================================================

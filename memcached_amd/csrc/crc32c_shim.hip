@@ -54,7 +54,9 @@ constexpr uint32_t kItemsPerBlockStep = 32;     // one span per 32-lane group
 constexpr uint32_t kFixedLen = 4096;            // K1 instance: 4 rows x 32 lanes x 32 B
 constexpr uint32_t kFixedCH = 32;
 static_assert(kFixedCH == mcrc_dev::kSpanCH, "K1 and the span kernels share one table image");
-#define K1_KERNEL mcrc_dev::k_fixed<4, 32, kFixedCH, 4, 5>
+// K1: MODE 11 (crc_in injected into the first data dword), loads fenced at the
+// top of each step; CRCIN selects the instance that reads crc_in[].
+#define K1_KERNEL(CRCIN) mcrc_dev::k_fixed<4, 32, kFixedCH, 4, 11, 2, 0, 0, true, CRCIN>
 
 thread_local float g_last_kernel_ms = -1.0f;
 
@@ -186,7 +188,9 @@ int init_device(Device &d, int id) {
     HIP_OK(hipEventCreate(&d.ev0));
     HIP_OK(hipEventCreate(&d.ev1));
     HIP_OK(hipEventCreateWithFlags(&d.busy, hipEventDisableTiming));
-    HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL(false), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               mcrc_dev::kLdsImage4Bytes));
+    HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL(true), hipFuncAttributeMaxDynamicSharedMemorySize,
                                mcrc_dev::kLdsImage4Bytes));
     const void *spans[] = {
         (const void *)mcrc_dev::k_spans<0, false>,
@@ -316,10 +320,15 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
     const bool fixed = s.offsets == nullptr && s.lens == nullptr;
     // every span has the same length whenever lens is absent (with or without offsets)
     const uint32_t kspan = s.lens == nullptr ? mcrc::xpow8n(s.len) : 0u;
-    if (fixed && s.len == kFixedLen && aligned16(s.base) && (s.stride & 15u) == 0) {
+    // (the lane offset within a step, item * stride, is 32-bit in K1)
+    if (fixed && s.len == kFixedLen && aligned16(s.base) && (s.stride & 15u) == 0 && s.stride < (1ull << 31)) {
         const uint32_t kfinal = ~mcrc::Gf2Op::zeros(s.len).apply(0xffffffffu);
-        hipLaunchKernelGGL((K1_KERNEL), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImage4Bytes, st,
-                           (const uint8_t *)s.base, s.stride, s.n, d.img_k1, kfinal, kspan, s.crc_in, s.out);
+        if (s.crc_in)
+            hipLaunchKernelGGL((K1_KERNEL(true)), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImage4Bytes,
+                               st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1, kfinal, kspan, s.crc_in, s.out);
+        else
+            hipLaunchKernelGGL((K1_KERNEL(false)), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImage4Bytes,
+                               st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1, kfinal, kspan, s.crc_in, s.out);
         return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
     }
     mcrc_dev::SpanArgs a{};

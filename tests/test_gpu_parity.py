@@ -56,6 +56,25 @@ def test_fixed_4096_k1(torch):
     np.testing.assert_array_equal(_u32(out), want_in)
 
 
+@pytest.mark.parametrize("n,stride", [(1, 4096), (2, 4096), (3, 8192), (33, 4096), (65, 12288), (8193, 4096)])
+def test_k1_edges(torch, n, stride):
+    """K1 at item counts that leave odd groups, partial steps and idle waves,
+    and at strides other than the item length; with and without crc_in."""
+    import ctypes
+    rng = np.random.default_rng(n)
+    host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    offs = np.arange(n, dtype=np.uint64) * stride
+    d = _dev(torch, host)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    cin = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dcin = _dev(torch, cin.view(np.int32))
+    for c in (None, cin):
+        s = _lib.Spans(d.data_ptr(), host.size, None, stride, None, 4096,
+                       None if c is None else dcin.data_ptr(), out.data_ptr(), n)
+        _lib.check(_lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None))
+        np.testing.assert_array_equal(_u32(out), oracle.batch(host, offs, np.full(n, 4096), c))
+
+
 def test_golden_all_lengths_alignments(torch):
     g = np.load(os.path.join(GOLD, "spans.npz"))
     buf = g["buf"]

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 
 #include "../memcached_amd/csrc/crc32c_gf2.h"
 #include "../memcached_amd/csrc/crc32c_host.h"
@@ -54,13 +55,19 @@ struct Variant {
     bool load_only;
     void (*kern)(const uint8_t *, uint64_t, uint64_t, const uint4 *, uint32_t, uint32_t,
                  const uint32_t *, uint32_t *);
+    bool needs_cin = false;  // kernel reads crc_in[] unconditionally (CRCIN instances)
+    uint32_t extra_lds = 0;
 };
 #define V(S, L, C, R, M) \
-    {#S "_l" #L "_c" #C "_r" #R "_m" #M, S, L, C, M == 1, mcrc_dev::k_fixed<S, L, C, R, M>}
+    {#S "_l" #L "_c" #C "_r" #R "_m" #M, S, L, C, (M == 1 || M >= 9), mcrc_dev::k_fixed<S, L, C, R, M>}
 #define VS(S, L, C, R, M, ST) \
-    {#S "_l" #L "_c" #C "_r" #R "_m" #M "_st" #ST, S, L, C, M == 1, mcrc_dev::k_fixed<S, L, C, R, M, 2, ST>}
+    {#S "_l" #L "_c" #C "_r" #R "_m" #M "_st" #ST, S, L, C, (M == 1 || M >= 9), mcrc_dev::k_fixed<S, L, C, R, M, 2, ST>}
 #define V3(S, L, C, R, M) \
-    {#S "_l" #L "_c" #C "_r" #R "_m" #M "_d3", S, L, C, M == 1, mcrc_dev::k_fixed<S, L, C, R, M, 3>}
+    {#S "_l" #L "_c" #C "_r" #R "_m" #M "_d3", S, L, C, (M == 1 || M >= 9), mcrc_dev::k_fixed<S, L, C, R, M, 3>}
+#define V11(F, CI) \
+    {"4_l32_c32_r4_m11_f" #F "_ci" #CI, 4, 32, 32, false, mcrc_dev::k_fixed<4, 32, 32, 4, 11, 2, 0, 0, F, CI>, CI}
+#define VP(S, L, C, R, M, D, P) \
+    {#S "_l" #L "_c" #C "_r" #R "_m" #M "_d" #D "_p" #P, S, L, C, (M == 1 || M >= 9), mcrc_dev::k_fixed<S, L, C, R, M, D, 0, P>}
 
 int main(int argc, char **argv) {
     const uint64_t nitems = argc > 1 ? strtoull(argv[1], 0, 0) : (1ull << 20);
@@ -68,6 +75,7 @@ int main(int argc, char **argv) {
     const int iters = argc > 2 ? atoi(argv[2]) : 10;
     const char *only = argc > 3 ? argv[3] : nullptr;  // substring filter on variant names
     const int only_bs = argc > 4 ? atoi(argv[4]) : 0;
+    const int reps = argc > 5 ? atoi(argv[5]) : 1;  // interleaved repetitions of the variant list
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     printf("device %s CUs %d\n", prop.name, prop.multiProcessorCount);
@@ -107,38 +115,50 @@ int main(int argc, char **argv) {
     }
 
     Variant vars[] = {
-        V(4, 32, 64, 2, 5), V(4, 32, 32, 4, 5), V(4, 32, 16, 8, 5), V(4, 32, 16, 8, 0),
-        V(4, 32, 16, 8, 3), V(4, 32, 32, 4, 3), V(4, 32, 16, 8, 1), V(4, 32, 64, 2, 1),
+        V(4, 32, 32, 4, 5), V11(true, false), V11(true, true), V(4, 32, 32, 4, 7), V(4, 32, 32, 4, 1),
+        V(4, 32, 32, 4, 10),
     };
+#ifdef MCRC_UBENCH_CLOCK
+    const int max_grid = prop.multiProcessorCount * 2;
+    uint64_t *d_stamps;
+    CK(hipMalloc(&d_stamps, max_grid * 4 * sizeof(uint64_t)));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(mcrc_dev::g_clock_stamps), &d_stamps, sizeof(d_stamps)));
+    int wall_khz = 0;
+    CK(hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, 0));
+    std::vector<uint64_t> stamps(max_grid * 4);
+#endif
     std::vector<uint32_t> img(mcrc::kImage4Dwords);
     uint4 *d_img;
     CK(hipMalloc(&d_img, mcrc::kImage4Dwords * 4));
     const uint32_t kfinal = ~mcrc::Gf2Op::zeros(len).apply(0xffffffffu);
     const uint32_t kspan = mcrc::xpow8n(len);
     std::vector<uint32_t> got(nitems);
+    for (int rep = 0; rep < reps; ++rep)
     for (const Variant &v : vars) {
-        if (only && !strstr(v.name, only)) continue;
+        if (only && only[0] && !strstr(v.name, only)) continue;
         uint32_t lds_bytes;
         if (v.slice == 1) {
             mcrc::build_lds_image1(img.data(), v.ch);
             lds_bytes = mcrc_dev::kLdsImage1Bytes;
         } else {
             mcrc::build_lds_image4(img.data(), v.ch);
-            lds_bytes = mcrc_dev::kLdsImage4Bytes;
+            lds_bytes = mcrc_dev::kLdsImage4Bytes + v.extra_lds;
         }
-        CK(hipMemcpy(d_img, img.data(), lds_bytes, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_img, img.data(), lds_bytes - v.extra_lds, hipMemcpyHostToDevice));
         CK(hipFuncSetAttribute((const void *)v.kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                lds_bytes));
         for (int pass = 0; pass < 3; ++pass) {
-            const bool with_crc_in = pass == 1;
+            const bool with_crc_in = pass == 1 || v.needs_cin;
+            if (v.needs_cin && pass == 1) continue;
             const bool hot = pass == 2;  // stride 0: every item is item 0 (cache-resident)
-            if (with_crc_in && (v.load_only || only_bs)) continue;
+            if (pass == 1 && (v.load_only || only_bs || reps > 1)) continue;
+            if (hot && rep > 0) continue;
             const uint64_t istride = hot ? 0 : len;
             const int bs = 1024;
             const int grid = prop.multiProcessorCount * (v.slice == 1 ? 2 : 1);
             std::vector<uint32_t> cin(nitems);
             uint32_t *d_cin = nullptr;
-            if (with_crc_in) {
+            if (with_crc_in || v.needs_cin) {
                 for (uint64_t i = 0; i < nitems; ++i) cin[i] = (uint32_t)(i * 2654435761u);
                 CK(hipMalloc(&d_cin, nitems * 4));
                 CK(hipMemcpy(d_cin, cin.data(), nitems * 4, hipMemcpyHostToDevice));
@@ -160,15 +180,28 @@ int main(int argc, char **argv) {
             if (!v.load_only) {
                 CK(hipMemcpy(got.data(), d_out, nitems * 4, hipMemcpyDeviceToHost));
                 for (uint64_t i = 0; i < nitems; ++i) {
-                    const uint32_t w = hot           ? want[0]
-                                       : with_crc_in ? mcrc::crc32c_host_hw(cin[i], &h_buf[i * len], len)
+                    const uint32_t w = with_crc_in ? mcrc::crc32c_host_hw(cin[i], &h_buf[hot ? 0 : i * len], len)
+                                       : hot         ? want[0]
                                                      : want[i];
                     bad += got[i] != w;
                 }
             }
-            printf("%-22s %s %8.3f ms  %8.1f GB/s  %5.1f%% of 8TB/s  bad=%llu\n", v.name,
-                   with_crc_in ? "crc_in" : hot ? "hot   " : "      ", ms, bytes / ms / 1e6,
-                   bytes / ms / 1e6 / 8000 * 100, (unsigned long long)bad);
+            double mhz = 0;
+#ifdef MCRC_UBENCH_CLOCK
+            {
+                CK(hipMemcpy(stamps.data(), d_stamps, grid * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+                std::vector<double> f;
+                for (int b = 0; b < grid; ++b) {
+                    const double dw = (double)(stamps[4 * b + 3] - stamps[4 * b + 2]);
+                    if (dw > 0) f.push_back((double)(stamps[4 * b + 1] - stamps[4 * b + 0]) / (dw / (wall_khz * 1e3)) / 1e6);
+                }
+                std::sort(f.begin(), f.end());
+                if (!f.empty()) mhz = f[f.size() / 2];
+            }
+#endif
+            printf("%-22s %s %8.3f ms  %8.1f GB/s  %5.1f%% of 8TB/s  bad=%llu  sclk~%.0f MHz\n", v.name,
+                   hot ? "hot   " : with_crc_in ? "crc_in" : "      ", ms, bytes / ms / 1e6,
+                   bytes / ms / 1e6 / 8000 * 100, (unsigned long long)bad, mhz);
             if (d_cin) CK(hipFree(d_cin));
         }
     }
