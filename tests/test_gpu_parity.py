@@ -501,3 +501,68 @@ def test_async_submit_wait():
     _lib.check(_lib.lib.crc32c_batch_submit(ctypes.byref(s), 0, ctypes.byref(job)))
     _lib.check(_lib.lib.crc32c_batch_wait(job))
     np.testing.assert_array_equal(out, oracle.batch(host, offs, lens))
+
+
+def _mixed_page(rng, n_items, wbuf, max_value):
+    items = [layout.make_item(b"m%06d" % i, rng.integers(0, 256, int(rng.integers(0, max_value)),
+                                                         dtype=np.uint8).tobytes(), cas=i + 1)
+             for i in range(n_items)]
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    soffs, slens = layout.spans_of(buf, offs)
+    layout.store_crcs(buf, offs, oracle.batch(buf, soffs, slens))
+    return buf, offs
+
+
+@pytest.mark.parametrize("max_value", [24, 700, 9000])
+def test_page_stream_tiny_to_large_items(torch, max_value):
+    """Item images from ~52 B (more than 32 spans per 4 KiB block) to ~9 KB,
+    verified and stamped through the page stream; flipped bits found exactly."""
+    rng = np.random.default_rng(max_value)
+    buf, offs = _mixed_page(rng, 3000, 1 << 20, max_value)
+    d = _dev(torch, buf)
+    ok, nbad = mc.verify_items(d, _dev(torch, offs.view(np.int64)), region_bytes=1 << 20)
+    assert nbad == 0 and ok.cpu().numpy().all()
+    victims = rng.choice(offs.size, 40, replace=False)
+    soffs, slens = layout.spans_of(buf, offs)
+    for v in victims:  # (past the header fields, so every span keeps its length)
+        buf[int(soffs[v] + rng.integers(16, slens[v]))] ^= 1 << int(rng.integers(0, 8))
+    ok, nbad = mc.verify_items(_dev(torch, buf), _dev(torch, offs.view(np.int64)), region_bytes=1 << 20)
+    want = np.ones(offs.size, np.uint8)
+    want[victims] = 0
+    assert nbad == victims.size
+    np.testing.assert_array_equal(ok.cpu().numpy(), want)
+    # stamp restores every CRC in place; the stamped buffer then verifies clean
+    d = _dev(torch, buf)
+    ok, nbad = mc.stamp_items(d, _dev(torch, offs.view(np.int64)), region_bytes=1 << 20)
+    assert nbad == 0 and ok.cpu().numpy().all()
+    stamped = d.cpu().numpy()
+    want_crc = oracle.batch(stamped, soffs, slens)
+    got_crc = np.array([int.from_bytes(stamped[int(o) + 28:int(o) + 32].tobytes(), "little") for o in offs],
+                       np.uint32)
+    np.testing.assert_array_equal(got_crc, want_crc)
+
+
+def test_page_stream_unsorted_offsets_bad_headers_and_tail(torch):
+    """Shuffled offsets, duplicated items, malformed headers and a buffer that
+    ends inside a 4 KiB block: the spans that cannot join the stream go
+    through the per-span kernel, the results are the oracle's."""
+    rng = np.random.default_rng(77)
+    buf, offs = _mixed_page(rng, 700, 1 << 20, 3000)
+    soffs, slens = layout.spans_of(buf, offs)
+    end = int(soffs[-1] + slens[-1])
+    buf = buf[: end + 5].copy()  # not a multiple of 4096: the last items are past the whole blocks
+    bad_hdr = rng.choice(offs.size, 7, replace=False)
+    for v in bad_hdr:
+        buf[int(offs[v]) + layout.NKEY_OFF] = 0  # nkey 0: malformed
+    flipped = np.setdiff1d(rng.choice(offs.size, 11, replace=False), bad_hdr)
+    for v in flipped:
+        buf[int(soffs[v] + slens[v] // 2)] ^= 0x10
+    order = rng.permutation(offs.size)
+    q = np.concatenate([offs[order], offs[order[:25]]])  # and 25 items listed twice
+    want = np.ones(offs.size, np.uint8)
+    want[bad_hdr] = 0
+    want[flipped] = 0
+    want_q = want[np.concatenate([order, order[:25]])]
+    ok, nbad = mc.verify_items(_dev(torch, buf), _dev(torch, q.view(np.int64)))
+    np.testing.assert_array_equal(ok.cpu().numpy(), want_q)
+    assert nbad == int((want_q == 0).sum())

@@ -20,5 +20,6 @@ for v in "$@"; do
     MCRC_LIB=$lib run 300 python bench.py --no-cpu-baseline --steps 30 > $O/c2_$v.json 2> $O/c2_$v.err
     MCRC_LIB=$lib run 300 python bench.py --workload config2r --steps 10 --warmup 2 > $O/c2r_$v.json 2> $O/c2r_$v.err
     MCRC_LIB=$lib run 300 python bench.py --workload config5 --pages 300 --steps 5 --warmup 1 > $O/c5_$v.json 2> $O/c5_$v.err
+    MCRC_LIB=$lib run 300 python bench.py --workload config3 --steps 5 --warmup 1 > $O/c3_$v.json 2> $O/c3_$v.err
 done
 echo done
