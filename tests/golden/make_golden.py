@@ -15,6 +15,11 @@ Outputs (committed):
   items.npz    memcached item images packed into wbufs (layout.py) with the
                spill CRC (storage.c:567) of every item: config-1 shaped items
                (key%07d, 4096-byte values, CAS) and items of varied geometry
+  config1.json BASELINE configs[0] in full (python tests/golden/make_golden.py
+               --config1): the 10 000 items tests/integration/extstore_config1.c
+               spills (value bytes: one splitmix64 stream, seed 1, 8 bytes per
+               draw), their spill CRCs' digest crc32c(0, CRCs as LE u32) and the
+               first and last CRCs
 """
 from __future__ import annotations
 
@@ -113,5 +118,36 @@ def main() -> None:
     print("wrote kat.json spans.npz items.npz")
 
 
+def config1() -> None:
+    """BASELINE configs[0]: 10 000 x (key%07d, 4096-byte value, CAS) spilled
+    into 4 MiB wbufs, CRCs from the reference crc32c.c."""
+    n, vlen = 10000, 4096
+    draws = n * vlen // 8
+    gamma = np.uint64(0x9E3779B97F4A7C15)
+    with np.errstate(over="ignore"):
+        z = np.uint64(1) + gamma * np.arange(1, draws + 1, dtype=np.uint64)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    values = z.astype("<u8").view(np.uint8).reshape(n, vlen)
+    items = [layout.make_item(b"key%07d" % i, values[i].tobytes(), cas=i + 1) for i in range(n)]
+    assert all(len(it) == 4165 for it in items)
+    buf, offs = layout.pack_wbufs(items, layout.WBUF_SIZE)
+    soffs, slens = layout.spans_of(buf, offs)
+    crcs = np.array([ref(0, buf[int(o):int(o) + int(ln)]) for o, ln in zip(soffs, slens)], np.uint32)
+    rec = {"items": n, "value_bytes": vlen, "ntotal": 4165, "wbuf": layout.WBUF_SIZE,
+           "wbufs": int(offs[-1] // layout.WBUF_SIZE) + 1, "items_per_wbuf": int((offs < layout.WBUF_SIZE).sum()),
+           "digest": ref(0, crcs.astype("<u4").tobytes()), "first_crcs": [int(c) for c in crcs[:8]],
+           "last_crcs": [int(c) for c in crcs[-8:]],
+           "source": "reference crc32c.c (oracle/_ref) after crc32c_init, hw == sw checked per item"}
+    with open(os.path.join(HERE, "config1.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+    print("wrote config1.json", rec["digest"])
+
+
 if __name__ == "__main__":
-    main()
+    if "--config1" in sys.argv:
+        config1()
+    else:
+        main()
+        config1()
