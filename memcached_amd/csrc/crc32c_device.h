@@ -117,6 +117,19 @@ __device__ __forceinline__ uint32_t step4_next(uint32_t x, uint32_t w_next, cons
     return xor3(xor3(a3, a2, a1), a0, w_next);
 }
 
+// K1 image (crc32c_gf2.h build_lds_image_k1): last-step tables of row chains
+// 0, 1, 2 with the row fold M_{(3-r)*1024} applied (4 plain tables each).
+constexpr uint32_t kAuxShift0 = 156, kAuxShift1 = 24, kAuxShift2 = 20;
+constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
+
+// Last slice-by-4 step of a row chain through the shifted tables t0..t0+3:
+// returns M_shift(T3[x0] ^ T2[x1] ^ T1[x2] ^ T0[x3]).
+__device__ __forceinline__ uint32_t step4_last_shifted(uint32_t x, uint32_t t0) {
+    return xor3(Step<4>::aux(t0, x & 0xffu), Step<4>::aux(t0 + 1, (x >> 8) & 0xffu),
+                Step<4>::aux(t0 + 2, (x >> 16) & 0xffu)) ^
+           Step<4>::aux(t0 + 3, x >> 24);
+}
+
 // Apply the zeros operator stored in aux tables t0..t0+3.
 template <int SLICE>
 __device__ __forceinline__ uint32_t apply_op(uint32_t t0, uint32_t v) {
@@ -162,6 +175,31 @@ __device__ __forceinline__ uint32_t group_reduce32_dpp(uint32_t v, uint32_t lane
                                                  Step<4>::aux(kAuxTree + 4 * K + 3, v >> 24);
         return group_reduce32_dpp<K + 1>(v, lane);
     }
+}
+
+// One level of the LPI = 32 reduction on the lanes selected by `on`.
+template <int K>
+__device__ __forceinline__ uint32_t reduce_level(uint32_t v, bool on) {
+    const uint32_t x = lane_down<K>(v);
+    if (on) v = xor3(Step<4>::aux(kAuxTree + 4 * K, v & 0xffu) ^ x, Step<4>::aux(kAuxTree + 4 * K + 1, (v >> 8) & 0xffu),
+                     Step<4>::aux(kAuxTree + 4 * K + 2, (v >> 16) & 0xffu)) ^
+                Step<4>::aux(kAuxTree + 4 * K + 3, v >> 24);
+    return v;
+}
+
+// Reduction of two items per 32-lane group (two consecutive steps of K1): a
+// holds item A's level-0 results on even lanes, b item B's on even lanes.
+// B's are moved to the odd lanes (DPP row_shr:1) and levels 1..4 run once for
+// both: at level k the lanes l with l % 2^(k+1) in {0, 1} merge with lane
+// l + 2^k, so A's raw CRC ends in lane 0 and B's in lane 1 of the group.
+// Saves four of the five levels of the second item's reduction.
+__device__ __forceinline__ uint32_t group_reduce32_pair(uint32_t a, uint32_t b, uint32_t lane) {
+    const uint32_t bs = __builtin_amdgcn_update_dpp(0u, b, 0x111, 0xf, 0xf, false);  // row_shr:1
+    uint32_t v = (lane & 1u) ? bs : a;
+    v = reduce_level<1>(v, (lane & 3u) < 2u);
+    v = reduce_level<2>(v, (lane & 7u) < 2u);
+    v = reduce_level<3>(v, (lane & 15u) < 2u);
+    return reduce_level<4>(v, (lane & 31u) < 2u);
 }
 
 // Copy a table image from global memory into this workgroup's LDS.

@@ -195,4 +195,28 @@ inline void build_lds_image4(uint32_t *img, uint32_t chunk) {
         }
 }
 
+// K1 image (160 KiB): the slice-by-4 image with the row fold absorbed into the
+// last dword step of the first three row chains.  Row r of a lane (R = 4 rows
+// of 32 * chunk bytes) must end up advanced by (3 - r) * 32 * chunk bytes; a
+// zeros operator is linear, so it can be applied to the step's table values
+// instead of to the chain's result:  S_r[j][b] = M_{(3-r)*32*chunk}(T_{3-j}[b])
+// (table j is indexed by byte j of the step input).  S_2 and S_1 replace aux
+// operators 5 and 6 (tables 20..27, unused by K1), S_0 takes tables 156..159
+// ([156 KiB, 160 KiB)).  crc32c_device.h kAuxShift* names the slots.
+constexpr int kImageK1Dwords = 160 * 256;
+
+inline void build_lds_image_k1(uint32_t *img, uint32_t chunk) {
+    build_lds_image4(img, chunk);
+    uint32_t t[4][256];
+    build_t0(t[0]);
+    for (int k = 1; k < 4; ++k)
+        for (int b = 0; b < 256; ++b) t[k][b] = t[0][t[k - 1][b] & 0xffu] ^ (t[k - 1][b] >> 8);
+    const int slot[3] = {156, 24, 20};  // tables of S_0, S_1, S_2
+    for (int r = 0; r < 3; ++r) {
+        const Gf2Op m = Gf2Op::zeros((uint64_t)(3 - r) * 32 * chunk);
+        for (int j = 0; j < 4; ++j)
+            for (int b = 0; b < 256; ++b) img[(slot[r] + j) * 256 + b] = m.apply(t[3 - j][b]);
+    }
+}
+
 }  // namespace mcrc

@@ -116,6 +116,31 @@ __device__ __forceinline__ uint32_t lane_partial_x3(const ItemRegs<32, CH, R> &i
     return a;
 }
 
+// lane_partial_x3 for R = 4 on the K1 image: the last step of row chains 0..2
+// reads the shifted tables (row fold included), so the lane partial is the
+// XOR of the four chains -- no fold operators.
+template <int CH>
+__device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &it, const LaneCtx &c) {
+    constexpr int Q = CH / 16;
+    constexpr int N = 4 * Q;  // dwords per chain
+    constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};
+    uint32_t x[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = it.d[r][0].x;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (i + 1 < N) {
+                x[r] = step4_next(x[r], dw4(it.d[r][(i + 1) >> 2], (i + 1) & 3), c);
+            } else {
+                x[r] = r < 3 ? step4_last_shifted(x[r], kShift[r]) : step4_next(x[r], 0u, c);
+            }
+        }
+    }
+    return xor3(x[0], x[1], x[2]) ^ x[3];
+}
+
 // Same as lane_partial_x3, but the loads of the NEXT step (into `nxt`) are
 // issued one at a time between dword steps of this chain, so the vector
 // memory queue is fed steadily instead of in one burst per step.
@@ -178,7 +203,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
                                                 const uint32_t *__restrict__ crc_in,
                                                 uint32_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    load_tables(smem, img, LdsImage<SLICE>::bytes);
+    load_tables(smem, img, MODE == 13 ? kLdsImageK1Bytes : LdsImage<SLICE>::bytes);
 #ifdef MCRC_UBENCH_CLOCK
     const uint64_t clk0 = clock64(), wall0 = wall_clock64();
 #endif
@@ -250,16 +275,19 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // live ranges), so the following step waits on loads issued moments before.
     auto ld = [&](ItemRegs<LPI, CH, R> &r, uint64_t gi) {
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
-        if constexpr (MODE == 11) {
+        if constexpr (MODE >= 11) {
             // uniform step base + per-lane offset: no 64-bit VGPR address math
             // (and no fresh temporaries) at the top of a step
             const uint64_t gu = gi < ngroups ? gi : ngroups - 1;
             const uint64_t first = gu * IPW;
             const uint8_t *wb = base + first * stride;
             const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
-            r.load_at(wb, gl * (uint32_t)stride + li * CH);
+            // crc_in first: it is consumed before the first chain step, and
+            // vmcnt counts in issue order (issued last, it made the step wait
+            // for all of its loads before any chain could start)
             if constexpr (CRCIN) r.cin = crc_in[first + gl];
             else r.cin = 0u;
+            r.load_at(wb, gl * (uint32_t)stride + li * CH);
         } else {
             r.load(addr(gi), li);
         }
@@ -284,6 +312,39 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
             grp += gstep;
             if (grp >= ngroups) break;
         }
+    } else if (DEPTH == 2 && (MODE == 12 || MODE == 13)) {
+        // MODE 11 with the two steps of an iteration reduced together
+        // (group_reduce32_pair): per item pair, 1 + 1 + 4 reduction levels
+        // instead of 2 x 5.  MODE 13: row folds inside the chains' last step
+        // (lane_partial_x3s, K1 image).
+        auto lp = [&](const ItemRegs<LPI, CH, R> &m) {
+            if constexpr (MODE == 13) return lane_partial_x3s<CH>(m, c);
+            else return lane_partial_x3<CH, R>(m, c);
+        };
+        auto part0 = [&](ItemRegs<LPI, CH, R> &m) {
+            if (li == 0) m.d[0][0].x ^= ~m.cin;
+            const uint32_t p = lp(m);
+            return reduce_level<0>(p, (lane & 1u) == 0u);
+        };
+        auto fin11 = [&](ItemRegs<LPI, CH, R> &m, uint64_t gi) {
+            if (li == 0) m.d[0][0].x ^= ~m.cin;
+            const uint32_t raw = group_reduce32_dpp(lp(m), lane);
+            const uint64_t item = item_of(gi);
+            if (li == 0 && item < nitems) out[item] = ~raw;
+        };
+        const uint64_t nsteps = (ngroups - grp + gstep - 1) / gstep;
+        ld(ra, grp);
+        for (uint64_t k = 0; k + 2 <= nsteps; k += 2) {
+            ld(rb, grp + gstep);
+            const uint32_t va = part0(ra);
+            ld(ra, grp + 2 * gstep);
+            const uint32_t vb = part0(rb);
+            const uint32_t raw = group_reduce32_pair(va, vb, lane);
+            const uint64_t item = item_of(li == 0 ? grp : grp + gstep);
+            if (li < 2 && item < nitems) out[item] = ~raw;
+            grp += 2 * gstep;
+        }
+        if (nsteps & 1) fin11(ra, grp);
     } else if (DEPTH == 2 && MODE == 11) {
         // One exit, at the bottom: a break between the two halves would give
         // the loop header a second (un-waited) predecessor, and the waitcnt

@@ -54,9 +54,10 @@ constexpr uint32_t kItemsPerBlockStep = 32;     // one span per 32-lane group
 constexpr uint32_t kFixedLen = 4096;            // K1 instance: 4 rows x 32 lanes x 32 B
 constexpr uint32_t kFixedCH = 32;
 static_assert(kFixedCH == mcrc_dev::kSpanCH, "K1 and the span kernels share one table image");
-// K1: MODE 11 (crc_in injected into the first data dword), loads fenced at the
-// top of each step; CRCIN selects the instance that reads crc_in[].
-#define K1_KERNEL(CRCIN) mcrc_dev::k_fixed<4, 32, kFixedCH, 4, 11, 2, 0, 0, true, CRCIN>
+// K1: MODE 13 (crc_in injected into the first data dword, row folds inside the
+// chains' last step via the K1 image, two steps reduced together), loads
+// fenced at the top of each step; CRCIN selects the instance that reads crc_in[].
+#define K1_KERNEL(CRCIN) mcrc_dev::k_fixed<4, 32, kFixedCH, 4, 13, 2, 0, 0, true, CRCIN>
 
 thread_local float g_last_kernel_ms = -1.0f;
 
@@ -65,7 +66,7 @@ struct Device {
     int cus = 0;
     bool ok = false;
     uint4 *img = nullptr;       // LDS table image (CH = 32) for every kernel
-    uint4 *img_k1 = nullptr;    // alias of img
+    uint4 *img_k1 = nullptr;    // K1 image (160 KiB, crc32c_gf2.h build_lds_image_k1)
     uint32_t *xpow = nullptr;   // 3 x 1024 x^(8n) table
     uint4 *zero = nullptr;      // 16 zero bytes
     unsigned long long *nbad = nullptr;
@@ -166,7 +167,10 @@ int init_device(Device &d, int id) {
     for (uint32_t t = 0; t < 16; ++t) xp[3072 + t] = mcrc::xpow8n_inv(t);
     HIP_OK(hipMalloc(&d.img, img.size() * 4));
     HIP_OK(hipMemcpy(d.img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
-    d.img_k1 = d.img;  // K1 and the span kernels share the CH = 32 image
+    std::vector<uint32_t> img_k1(mcrc::kImageK1Dwords);
+    mcrc::build_lds_image_k1(img_k1.data(), kFixedCH);
+    HIP_OK(hipMalloc(&d.img_k1, img_k1.size() * 4));
+    HIP_OK(hipMemcpy(d.img_k1, img_k1.data(), img_k1.size() * 4, hipMemcpyHostToDevice));
     std::vector<uint32_t> sp(512 * 32);
     for (uint32_t k = 0; k < 256; ++k) {
         const uint32_t lo = mcrc::xpow8n((uint64_t)mcrc_dev::kSegBytes * k);
@@ -189,9 +193,9 @@ int init_device(Device &d, int id) {
     HIP_OK(hipEventCreate(&d.ev1));
     HIP_OK(hipEventCreateWithFlags(&d.busy, hipEventDisableTiming));
     HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL(false), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               mcrc_dev::kLdsImage4Bytes));
+                               mcrc_dev::kLdsImageK1Bytes));
     HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL(true), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               mcrc_dev::kLdsImage4Bytes));
+                               mcrc_dev::kLdsImageK1Bytes));
     const void *spans[] = {
         (const void *)mcrc_dev::k_spans<0, false>,
         (const void *)mcrc_dev::k_spans<0, true>,
@@ -324,10 +328,10 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
     if (fixed && s.len == kFixedLen && aligned16(s.base) && (s.stride & 15u) == 0 && s.stride < (1ull << 31)) {
         const uint32_t kfinal = ~mcrc::Gf2Op::zeros(s.len).apply(0xffffffffu);
         if (s.crc_in)
-            hipLaunchKernelGGL((K1_KERNEL(true)), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImage4Bytes,
+            hipLaunchKernelGGL((K1_KERNEL(true)), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
                                st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1, kfinal, kspan, s.crc_in, s.out);
         else
-            hipLaunchKernelGGL((K1_KERNEL(false)), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImage4Bytes,
+            hipLaunchKernelGGL((K1_KERNEL(false)), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
                                st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1, kfinal, kspan, s.crc_in, s.out);
         return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
     }

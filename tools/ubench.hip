@@ -57,6 +57,7 @@ struct Variant {
                  const uint32_t *, uint32_t *);
     bool needs_cin = false;  // kernel reads crc_in[] unconditionally (CRCIN instances)
     uint32_t extra_lds = 0;
+    bool k1img = false;  // MODE 13: the 160 KiB K1 image (shifted last-step tables)
 };
 #define V(S, L, C, R, M) \
     {#S "_l" #L "_c" #C "_r" #R "_m" #M, S, L, C, (M == 1 || M >= 9), mcrc_dev::k_fixed<S, L, C, R, M>}
@@ -66,6 +67,10 @@ struct Variant {
     {#S "_l" #L "_c" #C "_r" #R "_m" #M "_d3", S, L, C, (M == 1 || M >= 9), mcrc_dev::k_fixed<S, L, C, R, M, 3>}
 #define V11(F, CI) \
     {"4_l32_c32_r4_m11_f" #F "_ci" #CI, 4, 32, 32, false, mcrc_dev::k_fixed<4, 32, 32, 4, 11, 2, 0, 0, F, CI>, CI}
+#define V12(F, CI) \
+    {"4_l32_c32_r4_m12_f" #F "_ci" #CI, 4, 32, 32, false, mcrc_dev::k_fixed<4, 32, 32, 4, 12, 2, 0, 0, F, CI>, CI}
+#define V13(F, CI) \
+    {"4_l32_c32_r4_m13_f" #F "_ci" #CI, 4, 32, 32, false, mcrc_dev::k_fixed<4, 32, 32, 4, 13, 2, 0, 0, F, CI>, CI, 0, true}
 #define VP(S, L, C, R, M, D, P) \
     {#S "_l" #L "_c" #C "_r" #R "_m" #M "_d" #D "_p" #P, S, L, C, (M == 1 || M >= 9), mcrc_dev::k_fixed<S, L, C, R, M, D, 0, P>}
 
@@ -115,8 +120,9 @@ int main(int argc, char **argv) {
     }
 
     Variant vars[] = {
-        V(4, 32, 32, 4, 5), V11(true, false), V11(true, true), V(4, 32, 32, 4, 7), V(4, 32, 32, 4, 1),
-        V(4, 32, 32, 4, 10),
+        V11(true, false), V12(true, false), V13(true, false), V11(true, true), V12(true, true), V13(true, true),
+        V(4, 32, 32, 4, 7),
+        V(4, 32, 32, 4, 1),
     };
 #ifdef MCRC_UBENCH_CLOCK
     const int max_grid = prop.multiProcessorCount * 2;
@@ -127,9 +133,9 @@ int main(int argc, char **argv) {
     CK(hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, 0));
     std::vector<uint64_t> stamps(max_grid * 4);
 #endif
-    std::vector<uint32_t> img(mcrc::kImage4Dwords);
+    std::vector<uint32_t> img(mcrc::kImageK1Dwords);
     uint4 *d_img;
-    CK(hipMalloc(&d_img, mcrc::kImage4Dwords * 4));
+    CK(hipMalloc(&d_img, mcrc::kImageK1Dwords * 4));
     const uint32_t kfinal = ~mcrc::Gf2Op::zeros(len).apply(0xffffffffu);
     const uint32_t kspan = mcrc::xpow8n(len);
     std::vector<uint32_t> got(nitems);
@@ -140,6 +146,9 @@ int main(int argc, char **argv) {
         if (v.slice == 1) {
             mcrc::build_lds_image1(img.data(), v.ch);
             lds_bytes = mcrc_dev::kLdsImage1Bytes;
+        } else if (v.k1img) {
+            mcrc::build_lds_image_k1(img.data(), v.ch);
+            lds_bytes = mcrc_dev::kLdsImageK1Bytes;
         } else {
             mcrc::build_lds_image4(img.data(), v.ch);
             lds_bytes = mcrc_dev::kLdsImage4Bytes + v.extra_lds;
