@@ -276,8 +276,10 @@ def traffic_per_launch():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # defaults: 50 timed launches after 20 untimed ones -- the core clock takes
+    # ~20 launches to settle (profiles/r01_ablations/k1_clock_ramp_800_launches.log)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--items", type=int, default=ITEMS_PER_GPU, help="items per GPU (default: config 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="config2",
@@ -324,7 +326,7 @@ def main():
         "data": "synthetic (torch.randint bytes, seed 42 + rank), device-resident",
         "config": {
             "workload": "BASELINE configs[1]: 1 Mi items x 4096 B per GPU, stride 4096, one 32-lane group per "
-                        "item (K1 k_fixed<slice-by-4, 32 lanes, 32 B/lane/row, 4 rows, bitop3 + DPP merge>)",
+                        "item (K1 k_fixed<slice-by-4, 32 lanes, 32 B/lane/row, 4 rows, row folds in the last-step tables, two items reduced per tree>)",
             "items_per_gpu": n,
             "item_bytes": ITEM_BYTES,
             "parallelism": f"items sharded across {world} rank(s), no collective on the data path",
