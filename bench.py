@@ -93,23 +93,51 @@ def timed(step, steps: int, world: int, sync=torch.cuda.synchronize):
     return max_over_ranks(time.perf_counter() - t0, world), r
 
 
-def make_batch(n: int, seed: int):
-    g = torch.Generator(device="cuda").manual_seed(seed)
-    data = torch.randint(0, 256, (n * ITEM_BYTES,), dtype=torch.uint8, device="cuda", generator=g)
+def splitmix64_bytes(nbytes: int, seed: int, chunk_words: int = 1 << 26, device: str = "cuda") -> torch.Tensor:
+    """SURVEY.md 8(d) config 2 input: little-endian splitmix64(seed) words,
+    word i = mix(seed + (i + 1) * golden), generated on the device in chunks."""
+    assert nbytes % 8 == 0
+    words = torch.empty(nbytes // 8, dtype=torch.int64, device=device)
+    golden = 0x9E3779B97F4A7C15 - (1 << 64)  # as int64 (wrapping arithmetic)
+    m1, m2 = 0xBF58476D1CE4E5B9 - (1 << 64), 0x94D049BB133111EB - (1 << 64)
+
+    def srl(x, k):  # logical shift right on int64
+        return (x >> k) & ((1 << (64 - k)) - 1)
+
+    for lo in range(0, words.numel(), chunk_words):
+        hi = min(lo + chunk_words, words.numel())
+        z = torch.arange(lo + 1, hi + 1, dtype=torch.int64, device=device) * golden + seed
+        z = (z ^ srl(z, 30)) * m1
+        z = (z ^ srl(z, 27)) * m2
+        words[lo:hi] = z ^ srl(z, 31)
+    return words.view(torch.uint8)
+
+
+def make_batch(n: int, seed: int, fill: str = "splitmix"):
+    if fill == "splitmix":
+        data = splitmix64_bytes(n * ITEM_BYTES, seed)
+    else:
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        data = torch.randint(0, 256, (n * ITEM_BYTES,), dtype=torch.uint8, device="cuda", generator=g)
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     spans = _lib.Spans(data.data_ptr(), data.numel(), None, ITEM_BYTES, None, ITEM_BYTES, None,
                        out.data_ptr(), n)
     return data, out, spans
 
 
-def run_steps(spans, steps: int, stream):
-    """Enqueue `steps` launches back to back on `stream`, one event pair each."""
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+def run_steps(spans, steps: int, stream, per_launch: bool = False):
+    """Enqueue `steps` launches back to back on `stream`.  Events: one pair
+    around all of them (default; sum of elapsed / steps = average launch
+    duration), or one pair per launch (`per_launch`)."""
     flags = _lib.CRC32C_DEVICE | _lib.CRC32C_ASYNC
-    for a, b in evs:
-        a.record(stream)
+    npairs = steps if per_launch else 1
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(npairs)]
+    for i in range(steps):
+        if per_launch or i == 0:
+            evs[i if per_launch else 0][0].record(stream)
         _lib.check(_lib.lib.crc32c_batch(ctypes.byref(spans), flags, ctypes.c_void_p(stream.cuda_stream)))
-        b.record(stream)
+        if per_launch or i == steps - 1:
+            evs[i if per_launch else 0][1].record(stream)
     return evs
 
 
@@ -282,6 +310,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--items", type=int, default=ITEMS_PER_GPU, help="items per GPU (default: config 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--events", default="region", choices=["region", "launch"],
+                    help="HIP events around the timed launches (region) or around each launch")
+    ap.add_argument("--fill", default="splitmix", choices=["splitmix", "randint"],
+                    help="item bytes: splitmix64(42 + rank) words (SURVEY.md 8d) or torch.randint")
     ap.add_argument("--workload", default="config2",
                     choices=["config2", "config2r", "config3", "config5", "pages", "stamp", "host"],
                     help="config2 = headline; others are extra measurements (not the bench line)")
@@ -294,7 +326,7 @@ def main():
     if _lib.lib.crc32c_gpu_count() < 1:
         raise SystemExit("libmcrc32c.so sees no gfx950 device")
     n = args.items
-    data, out, spans = make_batch(n, seed=42 + rank)
+    data, out, spans = make_batch(n, seed=42 + rank, fill=args.fill)
     stream = torch.cuda.current_stream()
 
     # warmup (also initialises the library's device state and tables)
@@ -302,9 +334,10 @@ def main():
         pass
     torch.cuda.synchronize()
 
-    elapsed, evs = timed(lambda k: run_steps(spans, k, stream), args.steps, world)
+    per_launch = args.events == "launch"
+    elapsed, evs = timed(lambda k: run_steps(spans, k, stream, per_launch), args.steps, world)
 
-    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     kernel_ms = max_over_ranks(kernel_ms, world)
     bytes_per_launch = n * ITEM_BYTES
     total_bytes = bytes_per_launch * args.steps * world
@@ -323,7 +356,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (torch.randint bytes, seed 42 + rank), device-resident",
+        "data": f"synthetic ({args.fill} bytes, seed 42 + rank), device-resident",
         "config": {
             "workload": "BASELINE configs[1]: 1 Mi items x 4096 B per GPU, stride 4096, one 32-lane group per "
                         "item (K1 k_fixed<slice-by-4, 32 lanes, 32 B/lane/row, 4 rows, row folds in the last-step tables, two items reduced per tree>)",
@@ -362,7 +395,7 @@ def extra_workload(args):
         run_steps(spans, max(1, args.warmup), stream)
         torch.cuda.synchronize()
         elapsed, evs = timed(lambda k: run_steps(spans, k, stream), args.steps, world)
-        kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        kms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
         res.update(config=cfg, kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
                    hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
     elif args.workload == "config5":
@@ -386,7 +419,7 @@ def extra_workload(args):
         run_steps(spans, max(1, args.warmup), stream)
         torch.cuda.synchronize()
         elapsed, evs = timed(lambda k: run_steps(spans, k, stream), args.steps, world)
-        kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        kms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
         nbytes = n * 4133
         res.update(config={"workload": f"config 2 variant: {n} x 4133-B spans at stride 4165, start +32 "
                                        "(K2, one unit per span)"},
