@@ -359,7 +359,7 @@ def main():
         "data": f"synthetic ({args.fill} bytes, seed 42 + rank), device-resident",
         "config": {
             "workload": "BASELINE configs[1]: 1 Mi items x 4096 B per GPU, stride 4096, one 32-lane group per "
-                        "item (K1 k_fixed<slice-by-4, 32 lanes, 32 B/lane/row, 4 rows, row folds in the last-step tables, two items reduced per tree>)",
+                        "item (K1 k_fixed<slice-by-4, 32 lanes, 32 B/lane/row, 4 rows, row folds in the last-step tables, four items reduced per tree>)",
             "items_per_gpu": n,
             "item_bytes": ITEM_BYTES,
             "parallelism": f"items sharded across {world} rank(s), no collective on the data path",

@@ -202,6 +202,24 @@ __device__ __forceinline__ uint32_t group_reduce32_pair(uint32_t a, uint32_t b, 
     return reduce_level<4>(v, (lane & 31u) < 2u);
 }
 
+// Level 1 of two items' reductions (A on lanes 0 mod 4, B on lanes 1 mod 4
+// afterwards), for group_reduce32_quad.
+__device__ __forceinline__ uint32_t group_pair_level1(uint32_t a, uint32_t b, uint32_t lane) {
+    const uint32_t bs = __builtin_amdgcn_update_dpp(0u, b, 0x111, 0xf, 0xf, false);  // row_shr:1
+    return reduce_level<1>((lane & 1u) ? bs : a, (lane & 3u) < 2u);
+}
+
+// Four items per 32-lane group: ab and cd from group_pair_level1; cd moves up
+// two lanes (DPP row_shr:2) and levels 2..4 run once for all four, so items
+// A, B, C, D end in lanes 0, 1, 2, 3 of the group.
+__device__ __forceinline__ uint32_t group_reduce32_quad(uint32_t ab, uint32_t cd, uint32_t lane) {
+    const uint32_t cs = __builtin_amdgcn_update_dpp(0u, cd, 0x112, 0xf, 0xf, false);  // row_shr:2
+    uint32_t v = (lane & 2u) ? cs : ab;
+    v = reduce_level<2>(v, (lane & 7u) < 4u);
+    v = reduce_level<3>(v, (lane & 15u) < 4u);
+    return reduce_level<4>(v, (lane & 31u) < 4u);
+}
+
 // Copy a table image from global memory into this workgroup's LDS.
 __device__ __forceinline__ void load_tables(char *lds, const uint4 *__restrict__ img, uint32_t bytes) {
     uint4 *dst = reinterpret_cast<uint4 *>(lds);

@@ -203,7 +203,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
                                                 const uint32_t *__restrict__ crc_in,
                                                 uint32_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    load_tables(smem, img, MODE == 13 ? kLdsImageK1Bytes : LdsImage<SLICE>::bytes);
+    load_tables(smem, img, MODE >= 13 ? kLdsImageK1Bytes : LdsImage<SLICE>::bytes);
 #ifdef MCRC_UBENCH_CLOCK
     const uint64_t clk0 = clock64(), wall0 = wall_clock64();
 #endif
@@ -312,13 +312,14 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
             grp += gstep;
             if (grp >= ngroups) break;
         }
-    } else if (DEPTH == 2 && (MODE == 12 || MODE == 13)) {
+    } else if (DEPTH == 2 && (MODE == 12 || MODE == 13 || MODE == 14)) {
         // MODE 11 with the two steps of an iteration reduced together
         // (group_reduce32_pair): per item pair, 1 + 1 + 4 reduction levels
         // instead of 2 x 5.  MODE 13: row folds inside the chains' last step
-        // (lane_partial_x3s, K1 image).
+        // (lane_partial_x3s, K1 image).  MODE 14: MODE 13 with four steps per
+        // iteration reduced together (group_reduce32_quad).
         auto lp = [&](const ItemRegs<LPI, CH, R> &m) {
-            if constexpr (MODE == 13) return lane_partial_x3s<CH>(m, c);
+            if constexpr (MODE >= 13) return lane_partial_x3s<CH>(m, c);
             else return lane_partial_x3<CH, R>(m, c);
         };
         auto part0 = [&](ItemRegs<LPI, CH, R> &m) {
@@ -334,7 +335,25 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
         };
         const uint64_t nsteps = (ngroups - grp + gstep - 1) / gstep;
         ld(ra, grp);
-        for (uint64_t k = 0; k + 2 <= nsteps; k += 2) {
+        uint64_t k = 0;
+        if constexpr (MODE == 14) {
+            for (; k + 4 <= nsteps; k += 4) {
+                ld(rb, grp + gstep);
+                const uint32_t va = part0(ra);
+                ld(ra, grp + 2 * gstep);
+                const uint32_t vb = part0(rb);
+                const uint32_t vab = group_pair_level1(va, vb, lane);
+                ld(rb, grp + 3 * gstep);
+                const uint32_t vc = part0(ra);
+                ld(ra, grp + 4 * gstep);
+                const uint32_t vd = part0(rb);
+                const uint32_t raw = group_reduce32_quad(vab, group_pair_level1(vc, vd, lane), lane);
+                const uint64_t item = item_of(grp + (li & 3u) * gstep);
+                if (li < 4 && item < nitems) out[item] = ~raw;
+                grp += 4 * gstep;
+            }
+        }
+        for (; k + 2 <= nsteps; k += 2) {
             ld(rb, grp + gstep);
             const uint32_t va = part0(ra);
             ld(ra, grp + 2 * gstep);

@@ -54,10 +54,10 @@ constexpr uint32_t kItemsPerBlockStep = 32;     // one span per 32-lane group
 constexpr uint32_t kFixedLen = 4096;            // K1 instance: 4 rows x 32 lanes x 32 B
 constexpr uint32_t kFixedCH = 32;
 static_assert(kFixedCH == mcrc_dev::kSpanCH, "K1 and the span kernels share one table image");
-// K1: MODE 13 (crc_in injected into the first data dword, row folds inside the
-// chains' last step via the K1 image, two steps reduced together), loads
+// K1: MODE 14 (crc_in injected into the first data dword, row folds inside the
+// chains' last step via the K1 image, four steps reduced together), loads
 // fenced at the top of each step; CRCIN selects the instance that reads crc_in[].
-#define K1_KERNEL(CRCIN) mcrc_dev::k_fixed<4, 32, kFixedCH, 4, 13, 2, 0, 0, true, CRCIN>
+#define K1_KERNEL(CRCIN) mcrc_dev::k_fixed<4, 32, kFixedCH, 4, 14, 2, 0, 0, true, CRCIN>
 
 thread_local float g_last_kernel_ms = -1.0f;
 

@@ -56,10 +56,14 @@ def test_fixed_4096_k1(torch):
     np.testing.assert_array_equal(_u32(out), want_in)
 
 
-@pytest.mark.parametrize("n,stride", [(1, 4096), (2, 4096), (3, 8192), (33, 4096), (65, 12288), (8193, 4096)])
+@pytest.mark.parametrize("n,stride", [(1, 4096), (2, 4096), (3, 8192), (33, 4096), (65, 12288), (8193, 4096),
+                                      (41160, 4096), (57347, 4096)])
 def test_k1_edges(torch, n, stride):
     """K1 at item counts that leave odd groups, partial steps and idle waves,
-    and at strides other than the item length; with and without crc_in."""
+    and at strides other than the item length; with and without crc_in.
+    On 256 CUs (4096 waves, 2 items per wave-step) 41160 items give waves of
+    6 and 5 steps, 57347 items waves of 8 and 7: every mix of the 4-step,
+    2-step and single-step reductions."""
     import ctypes
     rng = np.random.default_rng(n)
     host = rng.integers(0, 256, n * stride, dtype=np.uint8)

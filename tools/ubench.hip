@@ -71,6 +71,8 @@ struct Variant {
     {"4_l32_c32_r4_m12_f" #F "_ci" #CI, 4, 32, 32, false, mcrc_dev::k_fixed<4, 32, 32, 4, 12, 2, 0, 0, F, CI>, CI}
 #define V13(F, CI) \
     {"4_l32_c32_r4_m13_f" #F "_ci" #CI, 4, 32, 32, false, mcrc_dev::k_fixed<4, 32, 32, 4, 13, 2, 0, 0, F, CI>, CI, 0, true}
+#define V14(F, CI) \
+    {"4_l32_c32_r4_m14_f" #F "_ci" #CI, 4, 32, 32, false, mcrc_dev::k_fixed<4, 32, 32, 4, 14, 2, 0, 0, F, CI>, CI, 0, true}
 #define VP(S, L, C, R, M, D, P) \
     {#S "_l" #L "_c" #C "_r" #R "_m" #M "_d" #D "_p" #P, S, L, C, (M == 1 || M >= 9), mcrc_dev::k_fixed<S, L, C, R, M, D, 0, P>}
 
@@ -120,7 +122,7 @@ int main(int argc, char **argv) {
     }
 
     Variant vars[] = {
-        V11(true, false), V12(true, false), V13(true, false), V11(true, true), V12(true, true), V13(true, true),
+        V11(true, false), V13(true, false), V14(true, false), V11(true, true), V13(true, true), V14(true, true),
         V(4, 32, 32, 4, 7),
         V(4, 32, 32, 4, 1),
     };
