@@ -278,7 +278,15 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
         if constexpr (MODE >= 11) {
             // uniform step base + per-lane offset: no 64-bit VGPR address math
             // (and no fresh temporaries) at the top of a step
+            // A wave's last prefetch runs one step past its last group; it
+            // re-reads that group (just loaded, cache-hot) -- clamping every
+            // wave to the batch's last group made 4096 waves read the same
+            // 8 KiB at the end of the launch.
+#ifdef MCRC_K1_CLAMP_LAST  // (ablation: the old clamp)
             const uint64_t gu = gi < ngroups ? gi : ngroups - 1;
+#else
+            const uint64_t gu = gi < ngroups ? gi : gi - gstep < ngroups ? gi - gstep : ngroups - 1;
+#endif
             const uint64_t first = gu * IPW;
             const uint8_t *wb = base + first * stride;
             const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
