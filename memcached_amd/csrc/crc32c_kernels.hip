@@ -471,6 +471,11 @@ constexpr uint32_t kRowBytes = 32 * kSpanCH;  // 1024
 constexpr uint32_t kBlockBytes = 4 * kRowBytes;  // 4096
 constexpr uint32_t kSegBytes = 64 * 1024;
 constexpr uint32_t kWhole = 0xffffffffu;      // unit segment index: the whole span
+// Pieces outside a span are read from a zeroed buffer; workgroup b reads the
+// 16 B at zero + 4 KiB * (b % 256), so the workgroups' zero reads spread over
+// L2 channels instead of all landing on one line (cf. K1's last prefetch).
+constexpr uint32_t kZeroSlots = 256;
+constexpr uint64_t kZeroBytes = 4096ull * kZeroSlots;
 
 struct SpanArgs {
     const uint8_t *base;       // all spans live in [base, base + base_bytes)
@@ -487,7 +492,7 @@ struct SpanArgs {
     unsigned long long *nbad;  // MODE 1: count of mismatches (atomic)
     uint64_t n;                // spans (items)
     const uint32_t *xpow;      // x^(8*j), x^(8*1024*j), x^(8*2^20*j) (3 x 1024), x^(-8t) (16)
-    const uint4 *zero;         // 16 zero bytes in device memory
+    const uint4 *zero;         // kZeroBytes of zeros in device memory
     // work units (nullptr: unit u = span u, one segment)
     const struct UnitRec *units;
     const uint32_t *nunits;    // device-side unit count
@@ -812,7 +817,12 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
     uint32_t k = 0;    // block index inside cur
     uint32_t acc = 0;  // lane accumulator over the blocks of cur
     BlockWin w0, w1;
-    load_block(w0, cur, 0, li, a.zero);
+#ifdef MCRC_ZERO_SINGLE  // (ablation: one zero line for every workgroup)
+    const uint4 *zero = a.zero;
+#else
+    const uint4 *zero = a.zero + (blockIdx.x % kZeroSlots) * (4096 / 16);
+#endif
+    load_block(w0, cur, 0, li, zero);
 
     // Process the block held in `w` (block k of cur) after issuing the loads of
     // the group's next block into `wn`.  Returns false once this group is done.
@@ -820,10 +830,10 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         const bool last = k + 1 >= cur.niters;
         UnitDesc nd;
         if (!last) {
-            load_block(wn, cur, k + 1, li, a.zero);
+            load_block(wn, cur, k + 1, li, zero);
         } else {
             nd = decode_unit<MODE, UNITS>(a, nxt, lane);
-            load_block(wn, nd, 0, li, a.zero);
+            load_block(wn, nd, 0, li, zero);
         }
 
         if (cur.niters) {

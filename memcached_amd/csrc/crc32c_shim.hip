@@ -68,7 +68,7 @@ struct Device {
     uint4 *img = nullptr;       // LDS table image (CH = 32) for every kernel
     uint4 *img_k1 = nullptr;    // K1 image (160 KiB, crc32c_gf2.h build_lds_image_k1)
     uint32_t *xpow = nullptr;   // 3 x 1024 x^(8n) table
-    uint4 *zero = nullptr;      // 16 zero bytes
+    uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
     unsigned long long *nbad = nullptr;
     hipStream_t stream = nullptr, copy = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -184,8 +184,8 @@ int init_device(Device &d, int id) {
     HIP_OK(hipMemcpy(d.segpow, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&d.xpow, xp.size() * 4));
     HIP_OK(hipMemcpy(d.xpow, xp.data(), xp.size() * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMalloc(&d.zero, 64));
-    HIP_OK(hipMemset(d.zero, 0, 64));
+    HIP_OK(hipMalloc(&d.zero, mcrc_dev::kZeroBytes));
+    HIP_OK(hipMemset(d.zero, 0, mcrc_dev::kZeroBytes));
     HIP_OK(hipMalloc(&d.nbad, sizeof(unsigned long long)));
     HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
