@@ -570,3 +570,49 @@ def test_page_stream_unsorted_offsets_bad_headers_and_tail(torch):
     ok, nbad = mc.verify_items(_dev(torch, buf), _dev(torch, q.view(np.int64)))
     np.testing.assert_array_equal(ok.cpu().numpy(), want_q)
     assert nbad == int((want_q == 0).sum())
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_spans(torch, seed):
+    """Seeded fuzz of crc32c_batch: random (possibly overlapping) offsets, a
+    mix of tiny, ~4 KiB, multi-block and multi-segment lengths, random crc_in
+    or none, random base misalignment; compared with the oracle."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(1, 1500))
+    kind = rng.integers(0, 4, n)
+    lens = np.where(kind == 0, rng.integers(0, 64, n),
+                    np.where(kind == 1, rng.integers(4000, 4300, n),
+                             np.where(kind == 2, rng.integers(0, 20000, n), rng.integers(60000, 300000, n))))
+    lens = lens.astype(np.uint32)
+    size = int(lens.max()) + int(rng.integers(1, 1 << 20))
+    host = rng.integers(0, 256, size + 64, dtype=np.uint8)
+    offs = np.array([rng.integers(0, size - int(l) + 1) for l in lens], dtype=np.uint64)
+    cin = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if seed % 2 else None
+    want = oracle.batch(host, offs, lens, cin)
+    d = _dev(torch, host)
+    out = mc.batch(d, offsets=_dev(torch, offs.view(np.int64)), lens=_dev(torch, lens.view(np.int32)),
+                   crc_in=None if cin is None else _dev(torch, cin.view(np.int32)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), want)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_fuzz_k1_fixed(torch, seed):
+    """Seeded fuzz of the K1 path: 4 KiB items at random 16-B-multiple strides
+    and random counts (every mix of 4/2/1-step reductions), with and without
+    crc_in."""
+    import ctypes
+    rng = np.random.default_rng(2000 + seed)
+    n = int(rng.integers(1, 40000))
+    stride = 4096 + 16 * int(rng.integers(0, 64))
+    host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    offs = np.arange(n, dtype=np.uint64) * stride
+    d = _dev(torch, host)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    cin = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dcin = _dev(torch, cin.view(np.int32))
+    for c in (None, cin):
+        s = _lib.Spans(d.data_ptr(), host.size, None, stride, None, 4096,
+                       None if c is None else dcin.data_ptr(), out.data_ptr(), n)
+        _lib.check(_lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None))
+        np.testing.assert_array_equal(_u32(out), oracle.batch(host, offs, np.full(n, 4096), c))
