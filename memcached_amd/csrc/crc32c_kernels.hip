@@ -1046,13 +1046,18 @@ __global__ void k_chain(const uint32_t *iov_crc, const uint32_t *lens, uint32_t 
 // buffer is a sequence of wbuf-sized reads; in each, items are packed from
 // offset 0, nkey == 0 ends the wbuf, the next item is at + ITEM_ntotal, and the
 // walk stops when fewer than sizeof(item) = 48 bytes remain.  One thread per
-// wbuf (the walk is a dependent chain, one header round trip per item).
+// wbuf (the walk is a dependent chain; a round trip fetches kWalkSpec headers
+// at the last item's stride, one round trip per kWalkSpec equal-sized items).
 //   k_walk (slots != nullptr): count the items of wbuf w into cnt[w] and keep
 //     the first kWalkSlots offsets (relative to the wbuf) in slots[w][];
 //   k_walk_place: copy the kept offsets to offs[prefix[w] + i];
 //   k_walk (slots == nullptr, prefix != nullptr): re-walk only the wbufs that
 //     held more than kWalkSlots items, writing offsets >= kWalkSlots.
 constexpr uint32_t kWalkSlots = 2048;
+#ifndef MCRC_WALK_SPEC
+#define MCRC_WALK_SPEC 4
+#endif
+constexpr int kWalkSpec = MCRC_WALK_SPEC;  // headers fetched per round trip (stride prediction)
 
 __global__ void k_walk(const uint8_t *base, uint64_t bytes, uint64_t wbuf, uint64_t nw, uint32_t *cnt,
                        uint32_t *slots, const uint32_t *prefix, uint64_t *offs) {
@@ -1060,22 +1065,43 @@ __global__ void k_walk(const uint8_t *base, uint64_t bytes, uint64_t wbuf, uint6
          w += (uint64_t)gridDim.x * blockDim.x) {
         if (!slots && cnt[w] <= kWalkSlots) continue;  // second pass: overflowed wbufs only
         const uint64_t start = w * wbuf, size = bytes - start < wbuf ? bytes - start : wbuf;
-        uint64_t off = 0;
+        uint64_t off = 0, s = 0;  // s: stride of the last item walked
         uint32_t c = 0;
-        while (off + 48 <= size) {
-            const uint8_t *it = base + start + off;
-            // every header field is read before the nkey test: one round trip per item
-            const uint32_t nkey = it[41];
-            const uint32_t nbytes = ld_u32_unaligned(it + 32);
-            const uint32_t flags = it[38] | (it[39] << 8);
-            if (nkey == 0) break;  // zeroed tail of the wbuf
-            if (slots) {
-                if (c < kWalkSlots) slots[w * kWalkSlots + c] = (uint32_t)off;
-            } else if (c >= kWalkSlots) {
-                offs[prefix[w] + c] = start + off;
+        bool done = false;
+        while (!done && off + 48 <= size) {
+            // One round trip fetches the headers at off, off + s, off + 2s, ...
+            // (the last stride predicts the next ones).  A predicted header is
+            // used only when the walk, recomputed from the real fields, lands on
+            // it, so the result is the sequential walk's whatever the data.
+            uint32_t nkey[kWalkSpec], nbytes[kWalkSpec], flags[kWalkSpec];
+#pragma unroll
+            for (int j = 0; j < kWalkSpec; ++j) {
+                const uint64_t o = off + j * s;
+                nkey[j] = nbytes[j] = flags[j] = 0;
+                if (j == 0 || (s != 0 && o + 48 <= size)) {
+                    const uint8_t *it = base + start + o;
+                    nkey[j] = it[41];
+                    nbytes[j] = ld_u32_unaligned(it + 32);
+                    flags[j] = it[38] | (it[39] << 8);
+                }
             }
-            ++c;
-            off += 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) + ((flags & 2u) ? 8 : 0);
+            const uint64_t o0 = off, s0 = s;
+#pragma unroll
+            for (int j = 0; j < kWalkSpec; ++j) {
+                if (j > 0 && (s0 == 0 || off != o0 + j * s0)) break;  // prediction missed: reload at off
+                if (off + 48 > size || nkey[j] == 0) {  // end of the wbuf / zeroed tail
+                    done = true;
+                    break;
+                }
+                if (slots) {
+                    if (c < kWalkSlots) slots[w * kWalkSlots + c] = (uint32_t)off;
+                } else if (c >= kWalkSlots) {
+                    offs[prefix[w] + c] = start + off;
+                }
+                ++c;
+                s = 48ull + nkey[j] + 1 + nbytes[j] + ((flags[j] & 256u) ? 4 : 0) + ((flags[j] & 2u) ? 8 : 0);
+                off += s;
+            }
         }
         if (slots) cnt[w] = c;
     }

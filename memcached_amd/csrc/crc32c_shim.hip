@@ -747,10 +747,13 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, prefix, (int)nw + 1));
     void *scan = d->grow(kScrWalkScan, tmp);
     if (!cnt || !prefix || !scan) return CRC32C_ENOMEM;
-    const int gw = (int)std::min<uint64_t>((nw + 255) / 256, 1024);
+    // one walking thread per wbuf, 16 per workgroup: a page's walks spread over
+    // every CU (256-thread groups put 1000 pages' walks on 63 CUs)
+    constexpr int kWalkBlock = 16;
+    const int gw = (int)std::min<uint64_t>((nw + kWalkBlock - 1) / kWalkBlock, 65535);
     uint32_t *slots = (uint32_t *)d->grow(kScrWalkSlots, nw * mcrc_dev::kWalkSlots * 4);
     if (!slots) return CRC32C_ENOMEM;
-    hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(256), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt, slots,
+    hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(kWalkBlock), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt, slots,
                        (const uint32_t *)nullptr, (uint64_t *)nullptr);
     // prefix[nw] = total: scan nw + 1 counts with a zero appended
     uint32_t *cnt1 = (uint32_t *)d->grow(kScrWalkCnt1, (nw + 1) * 4);
@@ -772,7 +775,7 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     if (!doffs || !dok) return CRC32C_ENOMEM;
     hipLaunchKernelGGL(mcrc_dev::k_walk_place, dim3((int)std::min<uint64_t>(nw, 8192)), dim3(256), 0, st, wbuf_bytes,
                        nw, (const uint32_t *)cnt, (const uint32_t *)slots, (const uint32_t *)prefix, doffs);
-    hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(256), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt,
+    hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(kWalkBlock), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt,
                        (uint32_t *)nullptr, (const uint32_t *)prefix, doffs);
     mcrc_dev::SpanArgs a{};
     a.base = dbase;

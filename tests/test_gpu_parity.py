@@ -306,6 +306,43 @@ def test_verify_pages_device_walk(torch):
     assert nbad == len(bad_offs)
 
 
+def test_verify_pages_walk_stride_runs(torch):
+    """The device walk fetches several headers per round trip at the last
+    item's stride: runs of equal-sized items broken by other sizes, a header
+    whose nbytes was flipped (the walk diverges from the packed offsets), a
+    zeroed nkey mid-run, wbufs ending a few bytes after an item, a partial last
+    wbuf, and more than 2048 equal items per wbuf (the overflow re-walk) -- all
+    give exactly the sequential walk of storage.c:950-1070."""
+    rng = np.random.default_rng(43)
+    sizes = []
+    while len(sizes) < 6000:
+        run = int(rng.integers(1, 40))
+        sizes += [int(rng.choice([0, 1, 7, 100, 4096, 4097]))] * run
+    items = [layout.make_item(b"r%06d" % i, rng.integers(0, 256, n, dtype=np.uint8).tobytes(), cas=i + 1)
+             for i, n in enumerate(sizes)]
+    for wbuf in (1 << 20, 4165 * 9 + 47, 4165 * 9 + 48):
+        buf, offs = layout.pack_wbufs(items, wbuf)
+        buf = buf[:buf.size - wbuf // 3]  # partial last wbuf
+        want = _walk(buf, wbuf)
+        got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, buf), wbuf)
+        np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), want)
+    buf, offs = layout.pack_wbufs(items, 1 << 20)
+    ok, nbad = mc.stamp_items(buf, offs, region_bytes=1 << 20)
+    assert nbad == 0
+    buf[int(offs[1234]) + 33] ^= 0x01  # nbytes + 256: the walk leaves the packed offsets
+    buf[int(offs[3000]) + 41] = 0      # nkey == 0 mid-run
+    want = _walk(buf, 1 << 20)
+    got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, buf), 1 << 20)
+    np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), want)
+    # > 2048 equal items per wbuf
+    small = [layout.make_item(b"e%06d" % i, b"x" * 5, cas=i + 1) for i in range(12000)]
+    buf, offs = layout.pack_wbufs(small, 256 << 10)
+    assert np.bincount((offs // (256 << 10)).astype(np.int64)).max() > 2048
+    got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, buf), 256 << 10)
+    np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), offs)
+    assert nbad == int((got_ok.cpu().numpy() == 0).sum())
+
+
 def test_chained_iovs(torch):
     """Chunked items (storage.c:163-170): the CRC chained over an item's iovs
     (header from +32, then each chunk) equals crc32c(0, concatenation)."""
