@@ -1055,7 +1055,7 @@ __global__ void k_chain(const uint32_t *iov_crc, const uint32_t *lens, uint32_t 
 //     held more than kWalkSlots items, writing offsets >= kWalkSlots.
 constexpr uint32_t kWalkSlots = 2048;
 #ifndef MCRC_WALK_SPEC
-#define MCRC_WALK_SPEC 4
+#define MCRC_WALK_SPEC 8
 #endif
 constexpr int kWalkSpec = MCRC_WALK_SPEC;  // headers fetched per round trip (stride prediction)
 

@@ -749,7 +749,10 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     if (!cnt || !prefix || !scan) return CRC32C_ENOMEM;
     // one walking thread per wbuf, 16 per workgroup: a page's walks spread over
     // every CU (256-thread groups put 1000 pages' walks on 63 CUs)
-    constexpr int kWalkBlock = 16;
+#ifndef MCRC_WALK_BLOCK
+#define MCRC_WALK_BLOCK 16
+#endif
+    constexpr int kWalkBlock = MCRC_WALK_BLOCK;
     const int gw = (int)std::min<uint64_t>((nw + kWalkBlock - 1) / kWalkBlock, 65535);
     uint32_t *slots = (uint32_t *)d->grow(kScrWalkSlots, nw * mcrc_dev::kWalkSlots * 4);
     if (!slots) return CRC32C_ENOMEM;
