@@ -141,6 +141,22 @@ def run_steps(spans, steps: int, stream, per_launch: bool = False):
     return evs
 
 
+def settle(step, ms: float) -> int:
+    """Repeat `step` (in batches of 8) for `ms` of wall time before any
+    warmup or timed step.  After idle the MI355X clock ramps over the first
+    tens of launches (profiles/r01_ablations/k1_clock_ramp_800_launches.log:
+    the first 20 launches average 1-2 % slower than the steady state), so a
+    short warmup alone times part of the ramp.  Returns the launches run."""
+    if ms <= 0:
+        return 0
+    n, t0 = 0, time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        step(8)
+        torch.cuda.synchronize()
+        n += 8
+    return n
+
+
 def cpu_baseline(data: torch.Tensor, out: torch.Tensor):
     """Reference crc32c.c on host cores over a bounded sample of the batch."""
     ref = os.path.join(ROOT, "oracle", "_ref", "libref_crc32c.so")
@@ -308,6 +324,9 @@ def main():
     # ~20 launches to settle (profiles/r01_ablations/k1_clock_ramp_800_launches.log)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=250.0,
+                    help="before the warmup steps, repeat the step for this long (wall ms) so the GPU clock "
+                         "leaves its idle ramp; not counted as warmup or timed steps (0 = off)")
     ap.add_argument("--items", type=int, default=ITEMS_PER_GPU, help="items per GPU (default: config 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--events", default="region", choices=["region", "launch"],
@@ -329,7 +348,9 @@ def main():
     data, out, spans = make_batch(n, seed=42 + rank, fill=args.fill)
     stream = torch.cuda.current_stream()
 
-    # warmup (also initialises the library's device state and tables)
+    # clock settle, then the W warmup steps (the first launch also initialises
+    # the library's device state and tables)
+    settled = settle(lambda k: run_steps(spans, k, stream), args.settle_ms)
     for a, b in run_steps(spans, max(1, args.warmup), stream):
         pass
     torch.cuda.synchronize()
@@ -351,6 +372,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle": {"ms": args.settle_ms, "launches": settled},
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",

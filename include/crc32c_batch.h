@@ -45,6 +45,8 @@ extern "C" {
 #define CRC32C_EHIP (-2)   /* HIP runtime error */
 #define CRC32C_EINVAL (-3) /* bad arguments */
 #define CRC32C_ENOMEM (-4) /* device or pinned allocation failed */
+#define CRC32C_ERANGE (-5) /* a span lies outside [base, base + base_bytes): it was
+                              not read and its out[] entry is 0 */
 
 /* flags */
 #define CRC32C_DEVICE 0x1u    /* every pointer in the batch is device memory of the
@@ -56,7 +58,14 @@ extern "C" {
 /* A batch of byte spans inside one buffer.
  *   span i = [base + (offsets ? offsets[i] : i * stride),  + (lens ? lens[i] : len))
  *   out[i] = crc32c(crc_in ? crc_in[i] : 0, span i)
- * base_bytes bounds every span (host batches copy [0, base_bytes) lazily). */
+ * base_bytes bounds every span: no byte outside [base, base + base_bytes) is
+ * read.  A span that does not fit is skipped (out[i] = 0) and the call returns
+ * CRC32C_ERANGE (device batches with CRC32C_ASYNC cannot report it: their
+ * out-of-range spans still read nothing and get 0).  A batch of equal spans
+ * at a fixed stride that overruns base_bytes is rejected up front
+ * (CRC32C_EINVAL).  offsets / lens / crc_in / out hold n entries each.
+ * Spans may come in any order and may overlap (chunked-item iov lists keep
+ * their chain order; host batches are staged in offset order internally). */
 typedef struct crc32c_spans {
     const void *base;
     uint64_t base_bytes;
@@ -108,7 +117,11 @@ int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, u
  * next item at + ITEM_ntotal, stop when < 48 bytes remain) and every item
  * verified as crc32c_verify_items does (with region_bytes = wbuf_bytes).
  * *nitems = items found; the first min(cap, *nitems) offsets and ok flags are
- * written to offsets[] / ok[] (may be NULL when cap == 0), in walk order. */
+ * written to offsets[] / ok[], in walk order, and *nbad counts every bad item.
+ * cap == 0 is a count-only query: the walk runs, nothing is verified, *nbad =
+ * 0 and offsets / ok may be NULL.  An item count is at most
+ * base_bytes / 50 + ceil(base_bytes / wbuf_bytes) (an image is >= 50 bytes; a
+ * wbuf's last counted image may run past its end). */
 int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_bytes,
                         uint64_t *offsets, uint8_t *ok, uint64_t cap, uint64_t *nitems,
                         uint64_t *nbad, unsigned flags, void *stream);

@@ -63,6 +63,19 @@ def _ptr(x):
     return x.ctypes.data
 
 
+def _check_dev(t, name, n, dtypes):
+    """A device descriptor array: contiguous, on the device, one of `dtypes`
+    (names), at least n elements (the kernels read n of them unchecked)."""
+    import torch
+    if not (_is_torch(t) and t.is_cuda and t.is_contiguous()):
+        raise ValueError(f"{name}: device batches need a contiguous device tensor")
+    if str(t.dtype).replace("torch.", "") not in dtypes:
+        raise TypeError(f"{name}: dtype {t.dtype} (need one of {', '.join(dtypes)})")
+    if t.numel() < n:
+        raise ValueError(f"{name}: {t.numel()} elements for {n} spans")
+    return torch
+
+
 def batch(buf, offsets=None, stride: int = 0, lens=None, length: int = 0, crc_in=None, out=None,
           aligned16: bool = False, stream=None, asynchronous: bool = False):
     """Batched CRC-32C of spans of ``buf``.
@@ -81,11 +94,16 @@ def batch(buf, offsets=None, stride: int = 0, lens=None, length: int = 0, crc_in
         raise ValueError("need offsets or lens to know the batch size")
     if dev:
         import torch
+        if not buf.is_contiguous():
+            raise ValueError("buf: device batches need a contiguous device tensor")
         if out is None:
             out = torch.empty(n, dtype=torch.int32, device=buf.device)
-        for t in (offsets, lens, crc_in):
-            if t is not None and not (_is_torch(t) and t.is_cuda and t.is_contiguous()):
-                raise ValueError("device batches need contiguous device tensors")
+        _check_dev(out, "out", n, ("int32", "uint32"))
+        if offsets is not None:
+            _check_dev(offsets, "offsets", n, ("int64", "uint64"))
+        for name, t in (("lens", lens), ("crc_in", crc_in)):
+            if t is not None:
+                _check_dev(t, name, n, ("int32", "uint32"))
         base_bytes = buf.numel() * buf.element_size()
         if stream is None:
             stream = torch.cuda.current_stream(buf.device).cuda_stream
@@ -97,6 +115,11 @@ def batch(buf, offsets=None, stride: int = 0, lens=None, length: int = 0, crc_in
         crc_in = None if crc_in is None else np.ascontiguousarray(crc_in, dtype=np.uint32)
         if out is None:
             out = np.empty(n, dtype=np.uint32)
+        for name, a in (("lens", lens), ("crc_in", crc_in), ("out", out)):
+            if a is not None and a.size < n:
+                raise ValueError(f"{name}: {a.size} elements for {n} spans")
+        if out.dtype not in (np.uint32, np.int32) or not out.flags.c_contiguous:
+            raise TypeError("out: need a contiguous uint32 array")
     s = _lib.Spans(_ptr(buf), base_bytes, _ptr(offsets), stride, _ptr(lens), length, _ptr(crc_in),
                    _ptr(out), n)
     flags = (CRC32C_DEVICE if dev else 0) | (CRC32C_ALIGNED16 if aligned16 else 0)
@@ -131,6 +154,7 @@ def verify_items(buf, item_offsets, region_bytes=0, stream=None):
     if dev:
         import torch
         n = item_offsets.numel()
+        _check_dev(item_offsets, "item_offsets", n, ("int64", "uint64"))
         ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
         if stream is None:
             stream = torch.cuda.current_stream(buf.device).cuda_stream
@@ -156,6 +180,7 @@ def stamp_items(buf, item_offsets, region_bytes=0, stream=None):
     if dev:
         import torch
         n = item_offsets.numel()
+        _check_dev(item_offsets, "item_offsets", n, ("int64", "uint64"))
         ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
         if stream is None:
             stream = torch.cuda.current_stream(buf.device).cuda_stream
@@ -176,30 +201,41 @@ def stamp_items(buf, item_offsets, region_bytes=0, stream=None):
 
 def verify_pages(buf, wbuf_bytes, stream=None):
     """Walk every wbuf-sized read of ``buf`` on the device and verify each
-    item found.  Returns (item offsets, ok flags, nbad) in walk order."""
+    item found.  Returns (item offsets, ok flags, nbad) in walk order.
+
+    One library call when the items fit a first guess of the capacity
+    (images of >= 1 KiB on average); otherwise a second call with the exact
+    count the first one reported."""
     dev = _is_torch(buf) and buf.is_cuda
     nitems, nbad = ctypes.c_uint64(0), ctypes.c_uint64(0)
     if dev:
         import torch
+        if not buf.is_contiguous():
+            raise ValueError("buf: need a contiguous device tensor")
         if stream is None:
             stream = torch.cuda.current_stream(buf.device).cuda_stream
         nbytes = buf.numel() * buf.element_size()
-        check(lib.crc32c_verify_pages(buf.data_ptr(), nbytes, wbuf_bytes, None, None, 0, ctypes.byref(nitems),
-                                      ctypes.byref(nbad), CRC32C_DEVICE, stream), "crc32c_verify_pages")
-        n = nitems.value
-        offs = torch.empty(n, dtype=torch.int64, device=buf.device)
-        ok = torch.empty(n, dtype=torch.uint8, device=buf.device)
-        check(lib.crc32c_verify_pages(buf.data_ptr(), nbytes, wbuf_bytes, offs.data_ptr(), ok.data_ptr(), n,
-                                      ctypes.byref(nitems), ctypes.byref(nbad), CRC32C_DEVICE, stream),
-              "crc32c_verify_pages")
-        return offs, ok, int(nbad.value)
+        nw = -(-nbytes // wbuf_bytes)
+        cap = min(nbytes // 1024 + nw, nbytes // 50 + nw)
+        while True:
+            offs = torch.empty(cap, dtype=torch.int64, device=buf.device)
+            ok = torch.empty(cap, dtype=torch.uint8, device=buf.device)
+            check(lib.crc32c_verify_pages(buf.data_ptr(), nbytes, wbuf_bytes, offs.data_ptr(), ok.data_ptr(), cap,
+                                          ctypes.byref(nitems), ctypes.byref(nbad), CRC32C_DEVICE, stream),
+                  "crc32c_verify_pages")
+            n = nitems.value
+            if n <= cap:
+                return offs[:n], ok[:n], int(nbad.value)
+            cap = n
     buf = _host_buf(buf)
-    cap = buf.size // 50 + 1  # an image is at least 50 bytes
+    # an image is >= 50 bytes and each wbuf's last counted image may run past its end
+    cap = buf.size // 50 + -(-buf.size // wbuf_bytes)
     offs = np.empty(cap, np.uint64)
     ok = np.empty(cap, np.uint8)
     check(lib.crc32c_verify_pages(buf.ctypes.data, buf.size, wbuf_bytes, offs.ctypes.data, ok.ctypes.data, cap,
                                   ctypes.byref(nitems), ctypes.byref(nbad), 0, None), "crc32c_verify_pages")
     n = nitems.value
+    assert n <= cap, "item count above the proven bound"
     return offs[:n], ok[:n], int(nbad.value)
 
 
@@ -211,6 +247,11 @@ def batch_chains(buf, offsets, lens, chain_first, stream=None):
     n, nchains = len(offsets), len(chain_first) - 1
     if dev:
         import torch
+        if not buf.is_contiguous():
+            raise ValueError("buf: need a contiguous device tensor")
+        _check_dev(offsets, "offsets", n, ("int64", "uint64"))
+        _check_dev(lens, "lens", n, ("int32", "uint32"))
+        _check_dev(chain_first, "chain_first", nchains + 1, ("int64", "uint64"))
         iov_out = torch.empty(n, dtype=torch.int32, device=buf.device)
         out = torch.empty(nchains, dtype=torch.int32, device=buf.device)
         if stream is None:

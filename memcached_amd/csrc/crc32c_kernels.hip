@@ -489,7 +489,8 @@ struct SpanArgs {
     const uint32_t *crc_in;    // MODE 0: per-span initial CRC or nullptr (0)
     uint32_t *out;             // MODE 0: CRC per span
     uint8_t *ok;               // MODE 1: 1 if the stored CRC matches
-    unsigned long long *nbad;  // MODE 1: count of mismatches (atomic)
+    unsigned long long *nbad;  // MODE 1/2: count of mismatches / malformed images;
+                               // MODE 0: spans outside [base, base + base_bytes) (atomic)
     uint64_t n;                // spans (items)
     const uint32_t *xpow;      // x^(8*j), x^(8*1024*j), x^(8*2^20*j) (3 x 1024), x^(-8t) (16)
     const uint4 *zero;         // kZeroBytes of zeros in device memory
@@ -528,10 +529,12 @@ __device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
     ItemDesc d;
     const uint64_t off = a.offsets ? a.offsets[i] : i * a.stride;
     if (MODE == 0) {
-        d.p = a.base + off;
-        d.len = a.lens ? a.lens[i] : a.len;
+        // a span outside [base, base + base_bytes) is not read (out = 0, counted)
+        const uint32_t len = a.lens ? a.lens[i] : a.len;
+        d.sane = off <= a.base_bytes && len <= a.base_bytes - off;
+        d.p = a.base + (d.sane ? off : 0);
+        d.len = d.sane ? len : 0u;
         d.aux = a.crc_in ? a.crc_in[i] : 0u;
-        d.sane = true;
     } else {
         // item header fields (memcached.h:613-636), ITEM_ntotal (:149-152)
         const uint8_t *it = a.base + off;
@@ -629,7 +632,8 @@ __device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw,
     r.b = make_uint4(__shfl(raw, g | 4, 64), __shfl(raw, g | 5, 64), __shfl(raw, g | 6, 64), 0u);
     if (!UNITS && r.b.z) {
         const uint64_t off = r.a.x | ((uint64_t)r.a.y << 32);
-        r = make_unit(a.base, off, r.a.z, r.b.x, true, r.b.y, kWhole);
+        const bool sane = off <= a.base_bytes && r.a.z <= a.base_bytes - off;  // else: read nothing
+        r = make_unit(a.base, sane ? off : 0, sane ? r.a.z : 0u, r.b.x, sane, r.b.y, kWhole);
     }
     UnitDesc d;  // (aux and the span index stay in raw: read at the unit's end)
     d.p = a.base + (r.a.x | ((uint64_t)r.a.y << 32));
@@ -722,7 +726,8 @@ template <int MODE>
 __device__ __forceinline__ void emit(const SpanArgs &a, uint64_t item, uint32_t crc, uint32_t aux, bool sane,
                                      const uint8_t *p) {
     if (MODE == 0) {
-        a.out[item] = crc;
+        a.out[item] = sane ? crc : 0u;
+        if (!sane) atomicAdd(a.nbad, 1ull);  // span outside the buffer: not read
     } else if (MODE == 1) {
         const bool good = sane && crc == aux;
         a.ok[item] = good;

@@ -72,6 +72,7 @@ struct Device {
     unsigned long long *nbad = nullptr;
     hipStream_t stream = nullptr, copy = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};  // host-batch pipeline slots
     std::mutex mu;              // serialises every entry point on this device
     // Shared device scratch (plan buffers, nbad, walk buffers) is owned in
     // stream order: a launch on stream B waits for the last use on stream A.
@@ -192,6 +193,10 @@ int init_device(Device &d, int id) {
     HIP_OK(hipEventCreate(&d.ev0));
     HIP_OK(hipEventCreate(&d.ev1));
     HIP_OK(hipEventCreateWithFlags(&d.busy, hipEventDisableTiming));
+    for (int k = 0; k < 2; ++k) {
+        HIP_OK(hipEventCreateWithFlags(&d.copied[k], hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&d.done[k], hipEventDisableTiming));
+    }
     HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL(false), hipFuncAttributeMaxDynamicSharedMemorySize,
                                mcrc_dev::kLdsImageK1Bytes));
     HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL(true), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -319,8 +324,19 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
 }
 
 // Enqueue the kernels for a device-resident batch on `st`.
+// Equal spans at a fixed stride must fit [base, base + base_bytes): checked
+// here (the kernels read them unchecked).  Spans given by device offsets or
+// lengths are checked by the span kernels (out-of-range ones are not read).
+bool fixed_spans_fit(const crc32c_spans &s) {
+    if (s.offsets || s.lens) return true;
+    if (s.len > s.base_bytes) return false;
+    if (s.n <= 1 || s.stride == 0) return true;
+    return (s.n - 1) <= (s.base_bytes - s.len) / s.stride;
+}
+
 int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t st) {
     if (s.n == 0) return CRC32C_OK;
+    if (!fixed_spans_fit(s)) return CRC32C_EINVAL;
     const bool fixed = s.offsets == nullptr && s.lens == nullptr;
     // every span has the same length whenever lens is absent (with or without offsets)
     const uint32_t kspan = s.lens == nullptr ? mcrc::xpow8n(s.len) : 0u;
@@ -346,12 +362,28 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
         for (uint32_t t = 0; t < 16; ++t) a.kspan16[t] = mcrc::xpow8n((uint64_t)s.len + t);
     a.crc_in = s.crc_in;
     a.out = s.out;
+    a.nbad = d.nbad;  // spans outside the buffer
     a.n = s.n;
     a.xpow = d.xpow;
     a.zero = d.zero;
+    HIP_OK(hipMemsetAsync(d.nbad, 0, sizeof(unsigned long long), st));
     const bool aligned = (flags & CRC32C_ALIGNED16) ||
                          (fixed && aligned16(s.base) && (s.stride & 15u) == 0 && (s.len & 15u) == 0);
     return launch_units<0>(d, a, aligned, st);
+}
+
+// [p, p + bytes) lies inside one device allocation (so no kernel read bounded
+// by it can fault).  Memory the runtime cannot describe (e.g. host-registered
+// or managed) is not checked.
+bool device_range_ok(const void *p, uint64_t bytes) {
+    hipDeviceptr_t lo = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&lo, &size, (hipDeviceptr_t)p) != hipSuccess || lo == nullptr) {
+        (void)hipGetLastError();
+        return true;
+    }
+    const uint64_t skip = (uint64_t)((const uint8_t *)p - (const uint8_t *)lo);
+    return skip <= size && bytes <= size - skip;
 }
 
 bool is_pinned_or_device(const void *p) {
@@ -404,70 +436,87 @@ int ensure_slots(Device &d, uint64_t bytes, uint64_t items) {
 constexpr uint64_t kSlotBytes = 256ull << 20;  // bytes of span data per pipeline stage
 constexpr uint64_t kSlotItems = 1ull << 20;
 
-// Host-resident batch on one device.  Chunks of consecutive spans (offsets
-// must be non-decreasing) go through two pipeline slots: while chunk c is
-// checksummed, chunk c+1 is staged into pinned memory (unless the caller's
-// buffer is already pinned) and copied H2D on the copy stream.  Descriptors and
-// results travel through pinned twins so no copy touches pageable memory.
+// Host-resident batch on one device.  Spans are staged in offset order (a
+// permutation when the caller's order is not sorted: chunked-item iov lists
+// keep their chain order) in chunks that go through two pipeline slots: while
+// chunk c is checksummed, chunk c+1 is staged into pinned memory (unless the
+// caller's buffer is already pinned) and copied H2D on the copy stream.
+// Descriptors and results travel through pinned twins so no copy touches
+// pageable memory; results are scattered back to the caller's order.
 int run_host_batch(Device &d, const crc32c_spans &s) {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_OK(hipSetDevice(d.id));
-    d.acquire(d.stream);
-    d.acquire(d.copy);
-    struct Release {
-        Device &d;
-        ~Release() { d.release(d.stream); }
-    } release_on_exit{d};
     if (s.n == 0) return CRC32C_OK;
+    for (uint64_t i = 0; i < s.n; ++i) {
+        const uint64_t off = span_off(s, i), len = span_len(s, i);
+        if (off > s.base_bytes || len > s.base_bytes - off || len > kSlotBytes - 16) return CRC32C_EINVAL;
+    }
+    std::vector<uint64_t> order;  // staging order -> caller index (empty: identity)
     for (uint64_t i = 1; i < s.n; ++i)
-        if (span_off(s, i) < span_off(s, i - 1)) return CRC32C_EINVAL;
-    for (uint64_t i = 0; i < s.n; ++i)
-        if (span_off(s, i) + span_len(s, i) > s.base_bytes || span_len(s, i) > kSlotBytes - 16)
-            return CRC32C_EINVAL;
+        if (span_off(s, i) < span_off(s, i - 1)) {
+            order.resize(s.n);
+            for (uint64_t k = 0; k < s.n; ++k) order[k] = k;
+            std::stable_sort(order.begin(), order.end(),
+                             [&](uint64_t x, uint64_t y) { return span_off(s, x) < span_off(s, y); });
+            break;
+        }
+    auto idx = [&](uint64_t k) { return order.empty() ? k : order[k]; };
     int rc = ensure_slots(d, kSlotBytes, kSlotItems);
     if (rc) return rc;
+    d.acquire(d.stream);
+    d.acquire(d.copy);
+    // Every exit waits for both streams (an H2D copy may still be reading the
+    // caller's pinned buffer after an error) and hands the scratch on.
+    struct Guard {
+        Device &d;
+        ~Guard() {
+            (void)hipStreamSynchronize(d.copy);
+            (void)hipStreamSynchronize(d.stream);
+            d.release(d.stream);
+        }
+    } guard{d};
     const bool src_pinned = is_pinned_or_device(s.base);
     const uint8_t *src = (const uint8_t *)s.base;
-    hipEvent_t copied[2], done[2];
-    for (int k = 0; k < 2; ++k) {
-        HIP_OK(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
-        HIP_OK(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
-    }
-    uint64_t pend_i0[2] = {0, 0}, pend_n[2] = {0, 0};  // results waiting in hout[slot]
+    uint64_t pend_k0[2] = {0, 0}, pend_n[2] = {0, 0};  // results waiting in hout[slot]
     auto drain = [&](int k) -> int {
         if (!pend_n[k]) return CRC32C_OK;
-        HIP_OK(hipEventSynchronize(done[k]));
-        memcpy(s.out + pend_i0[k], d.hout[k], pend_n[k] * 4);
+        HIP_OK(hipEventSynchronize(d.done[k]));
+        if (order.empty()) memcpy(s.out + pend_k0[k], d.hout[k], pend_n[k] * 4);
+        else
+            for (uint64_t i = 0; i < pend_n[k]; ++i) s.out[order[pend_k0[k] + i]] = d.hout[k][i];
         pend_n[k] = 0;
         return CRC32C_OK;
     };
-    uint64_t i0 = 0;
+    uint64_t k0 = 0;
     int slot = 0;
-    while (i0 < s.n) {
-        const uint64_t lo = span_off(s, i0) & ~15ull;
-        uint64_t i1 = i0, hi = lo;
-        while (i1 < s.n && i1 - i0 < kSlotItems) {
-            const uint64_t e = span_off(s, i1) + span_len(s, i1);
+    while (k0 < s.n) {
+        const uint64_t lo = span_off(s, idx(k0)) & ~15ull;
+        uint64_t k1 = k0, hi = lo;
+        while (k1 < s.n && k1 - k0 < kSlotItems) {
+            const uint64_t e = span_off(s, idx(k1)) + span_len(s, idx(k1));
             if (std::max(hi, e) - lo > kSlotBytes) break;
             hi = std::max(hi, e);
-            ++i1;
+            ++k1;
         }
-        const uint64_t bytes = hi - lo, cnt = i1 - i0;
+        const uint64_t bytes = hi - lo, cnt = k1 - k0;
         if ((rc = drain(slot))) return rc;  // slot free: its kernel and D2H are done
         const uint8_t *h2d_src = src + lo;
         if (!src_pinned) {
             memcpy(d.pin[slot], src + lo, bytes);
             h2d_src = d.pin[slot];
         }
-        for (uint64_t i = 0; i < cnt; ++i) d.hoffs[slot][i] = span_off(s, i0 + i) - lo;
-        if (s.lens) memcpy(d.hlens[slot], s.lens + i0, cnt * 4);
-        if (s.crc_in) memcpy(d.hcin[slot], s.crc_in + i0, cnt * 4);
+        for (uint64_t i = 0; i < cnt; ++i) {
+            const uint64_t c = idx(k0 + i);
+            d.hoffs[slot][i] = span_off(s, c) - lo;
+            if (s.lens) d.hlens[slot][i] = s.lens[c];
+            if (s.crc_in) d.hcin[slot][i] = s.crc_in[c];
+        }
         HIP_OK(hipMemcpyAsync(d.dbuf[slot], h2d_src, bytes, hipMemcpyHostToDevice, d.copy));
         HIP_OK(hipMemcpyAsync(d.doffs[slot], d.hoffs[slot], cnt * 8, hipMemcpyHostToDevice, d.copy));
         if (s.lens) HIP_OK(hipMemcpyAsync(d.dlens[slot], d.hlens[slot], cnt * 4, hipMemcpyHostToDevice, d.copy));
         if (s.crc_in) HIP_OK(hipMemcpyAsync(d.dcin[slot], d.hcin[slot], cnt * 4, hipMemcpyHostToDevice, d.copy));
-        HIP_OK(hipEventRecord(copied[slot], d.copy));
-        HIP_OK(hipStreamWaitEvent(d.stream, copied[slot], 0));
+        HIP_OK(hipEventRecord(d.copied[slot], d.copy));
+        HIP_OK(hipStreamWaitEvent(d.stream, d.copied[slot], 0));
         crc32c_spans sub{};
         sub.base = d.dbuf[slot];
         sub.base_bytes = bytes;
@@ -479,17 +528,13 @@ int run_host_batch(Device &d, const crc32c_spans &s) {
         sub.n = cnt;
         if ((rc = enqueue_device(d, sub, 0, d.stream))) return rc;
         HIP_OK(hipMemcpyAsync(d.hout[slot], d.dout[slot], cnt * 4, hipMemcpyDeviceToHost, d.stream));
-        HIP_OK(hipEventRecord(done[slot], d.stream));
-        pend_i0[slot] = i0;
+        HIP_OK(hipEventRecord(d.done[slot], d.stream));
+        pend_k0[slot] = k0;
         pend_n[slot] = cnt;
-        i0 = i1;
+        k0 = k1;
         slot ^= 1;
     }
     if ((rc = drain(slot)) || (rc = drain(slot ^ 1))) return rc;
-    for (int k = 0; k < 2; ++k) {
-        (void)hipEventDestroy(copied[k]);
-        (void)hipEventDestroy(done[k]);
-    }
     return CRC32C_OK;
 }
 
@@ -508,9 +553,10 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
         if (nbad) *nbad = 0;
         return CRC32C_OK;
     }
-    std::lock_guard<std::mutex> lk(d->mu);
     hipStream_t st = (hipStream_t)stream;  // NULL: the default stream
     const bool dev = flags & CRC32C_DEVICE;
+    if (dev && !device_range_ok(base, base_bytes)) return CRC32C_EINVAL;
+    std::lock_guard<std::mutex> lk(d->mu);
     const uint8_t *dbase = (const uint8_t *)base;
     const uint64_t *doffs = item_offsets;
     uint8_t *dok = ok;
@@ -621,6 +667,7 @@ const char *crc32c_strerror(int err) {
         case CRC32C_EHIP: return "HIP runtime error";
         case CRC32C_EINVAL: return "invalid argument";
         case CRC32C_ENOMEM: return "out of device or pinned memory";
+        case CRC32C_ERANGE: return "span outside [base, base + base_bytes) (not read)";
         default: return "unknown error";
     }
 }
@@ -637,17 +684,29 @@ int crc32c_batch(const crc32c_spans *s, unsigned flags, void *stream) {
     // the kernel is ordered after whatever produced the buffers there.
     hipStream_t st = (hipStream_t)stream;
     const bool timed = !(flags & CRC32C_ASYNC);
+    if (s->n && !device_range_ok(s->base, s->base_bytes)) return CRC32C_EINVAL;
     std::lock_guard<std::mutex> lk(d->mu);
     d->acquire(st);
     if (timed) HIP_OK(hipEventRecord(d->ev0, st));
     rc = enqueue_device(*d, *s, flags, st);
-    d->release(st);
-    if (rc) return rc;
-    if (!timed) return CRC32C_OK;
+    if (rc) {
+        d->release(st);
+        return rc;
+    }
+    if (!timed) {
+        d->release(st);
+        return CRC32C_OK;
+    }
     HIP_OK(hipEventRecord(d->ev1, st));
+    // spans given by offsets / lengths are range-checked on the device
+    unsigned long long nrange = 0;
+    const bool checked = s->n && (s->offsets || s->lens);
+    if (checked) HIP_OK(hipMemcpyAsync(&nrange, d->nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
+    d->release(st);
     HIP_OK(hipEventSynchronize(d->ev1));
+    if (checked) HIP_OK(hipStreamSynchronize(st));
     (void)hipEventElapsedTime(&g_last_kernel_ms, d->ev0, d->ev1);
-    return CRC32C_OK;
+    return nrange ? CRC32C_ERANGE : CRC32C_OK;
 }
 
 int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, uint64_t nchains, uint32_t *out,
@@ -675,9 +734,13 @@ int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, u
     const uint32_t *crcs = iovs->out, *lens = iovs->lens;
     const uint64_t *first = chain_first;
     uint32_t *dout = out;
+    unsigned long long nrange = 0;
     if (dev) {
+        if (!device_range_ok(iovs->base, iovs->base_bytes)) return CRC32C_EINVAL;
         rc = enqueue_device(*d, *iovs, flags, st);
         if (rc) return rc;
+        if (!(flags & CRC32C_ASYNC) && (iovs->offsets || iovs->lens))  // range-checked on the device
+            HIP_OK(hipMemcpyAsync(&nrange, d->nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
     } else {  // stage the fold's inputs (small: 4-8 B per iov / chain)
         const uint64_t n = iovs->n;
         uint8_t *buf = (uint8_t *)d->grow(kScrStage, n * 8 + (nchains + 1) * 8 + nchains * 4 + 64);
@@ -699,7 +762,7 @@ int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, u
     HIP_OK(hipGetLastError());
     if (!dev) HIP_OK(hipMemcpyAsync(out, dout, nchains * 4, hipMemcpyDeviceToHost, st));
     if (!dev || !(flags & CRC32C_ASYNC)) HIP_OK(hipStreamSynchronize(st));
-    return CRC32C_OK;
+    return nrange ? CRC32C_ERANGE : CRC32C_OK;
 }
 
 int crc32c_verify_items(const void *base, uint64_t base_bytes, uint64_t region_bytes, const uint64_t *item_offsets,
@@ -720,9 +783,10 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     Device *d = nullptr;
     int rc = current_device(&d);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(d->mu);
     hipStream_t st = (hipStream_t)stream;
     const bool dev = flags & CRC32C_DEVICE;
+    if (dev && !device_range_ok(base, base_bytes)) return CRC32C_EINVAL;
+    std::lock_guard<std::mutex> lk(d->mu);
     const uint64_t nw = (base_bytes + wbuf_bytes - 1) / wbuf_bytes;
     d->acquire(st);
     struct Release {
@@ -768,7 +832,7 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     HIP_OK(hipMemcpyAsync(&total, prefix + nw, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     *nitems = total;
-    if (total == 0) {
+    if (total == 0 || cap == 0) {  // cap == 0: count-only query (no verify)
         *nbad = 0;
         return CRC32C_OK;
     }

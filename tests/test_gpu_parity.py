@@ -101,7 +101,10 @@ def test_golden_host_path():
     L, A = g["crc0"].shape
     offs = np.tile(np.arange(A, dtype=np.uint64), L)
     lens = np.repeat(np.arange(L, dtype=np.uint32), A)
-    order = np.argsort(offs, kind="stable")  # host batches need non-decreasing offsets
+    # caller order (offsets not sorted): the library stages in offset order and scatters back
+    out = mc.batch(g["buf"], offsets=offs, lens=lens, crc_in=g["cin"].reshape(-1))
+    np.testing.assert_array_equal(out, g["crcin"].reshape(-1))
+    order = np.argsort(offs, kind="stable")
     out = mc.batch(g["buf"], offsets=offs[order], lens=lens[order], crc_in=g["cin"].reshape(-1)[order])
     np.testing.assert_array_equal(out, g["crcin"].reshape(-1)[order])
 
@@ -365,7 +368,9 @@ def test_chained_iovs(torch):
                           _dev(torch, first.view(np.int64)))
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_u32(got), want)
-    # host path (iov offsets must be non-decreasing): the same chains over sorted iovs
+    # host path, iovs in chain order (not memory order), several pipeline slots
+    np.testing.assert_array_equal(mc.batch_chains(buf, offs, lens, first), want)
+    # and over sorted iovs
     offs_s = np.sort(offs)
     want_s = np.empty(nch, np.uint32)
     for c in range(nch):
@@ -653,3 +658,84 @@ def test_fuzz_k1_fixed(torch, seed):
                        None if c is None else dcin.data_ptr(), out.data_ptr(), n)
         _lib.check(_lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None))
         np.testing.assert_array_equal(_u32(out), oracle.batch(host, offs, np.full(n, 4096), c))
+
+
+def test_device_spans_outside_buffer_not_read(torch):
+    """Spans past base_bytes are skipped (out = 0) and reported as ERANGE; the
+    rest of the batch is exact.  Both the one-unit-per-span path (fixed
+    length) and the planned path (per-span lengths)."""
+    import ctypes
+    rng = np.random.default_rng(77)
+    host = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    d = _dev(torch, host)
+    n = 500
+    offs = rng.integers(0, host.size - 5000, n).astype(np.uint64)
+    bad = np.array([3, 77, 499])
+    offs[bad] = [host.size - 10, host.size + 4096, 1 << 62]
+    for lens in (np.full(n, 4133, np.uint32), rng.integers(0, 5000, n).astype(np.uint32)):
+        lens[bad[0]] = max(int(lens[bad[0]]), 11)  # ends past the buffer
+        good = np.ones(n, bool)
+        good[bad] = False
+        want = np.zeros(n, np.uint32)
+        want[good] = oracle.batch(host, offs[good], lens[good])
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+        dl = _dev(torch, lens.view(np.int32))
+        s = _lib.Spans(d.data_ptr(), host.size, _dev(torch, offs.view(np.int64)).data_ptr(), 0,
+                       dl.data_ptr() if lens.min() != lens.max() else None, int(lens[0]), None, out.data_ptr(), n)
+        rc = _lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None)
+        assert rc == _lib.CRC32C_ERANGE
+        np.testing.assert_array_equal(_u32(out), want)
+        # a batch without such spans reports OK again (the counter is per call)
+        s.n = 3
+        assert _lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None) == _lib.CRC32C_OK
+
+
+def test_fixed_stride_overrun_rejected(torch):
+    import ctypes
+    d = torch.zeros(10 * 4096, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(11, dtype=torch.int32, device="cuda")
+    s = _lib.Spans(d.data_ptr(), d.numel(), None, 4096, None, 4096, None, out.data_ptr(), 11)
+    assert _lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None) == _lib.CRC32C_EINVAL
+    s.n = 10
+    assert _lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None) == _lib.CRC32C_OK
+    # base_bytes larger than the allocation holding base
+    s.base_bytes = 1 << 40
+    assert _lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None) == _lib.CRC32C_EINVAL
+
+
+def test_python_device_descriptor_checks(torch):
+    d = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(TypeError):
+        mc.batch(d, offsets=torch.zeros(4, dtype=torch.int32, device="cuda"), length=16)
+    with pytest.raises(TypeError):
+        mc.batch(d, offsets=torch.zeros(4, dtype=torch.int64, device="cuda"),
+                 lens=torch.zeros(4, dtype=torch.int64, device="cuda"))
+    with pytest.raises(ValueError):
+        mc.batch(d, offsets=torch.zeros(4, dtype=torch.int64, device="cuda"),
+                 lens=torch.zeros(4, dtype=torch.int32, device="cuda"),
+                 out=torch.zeros(3, dtype=torch.int32, device="cuda"))
+    with pytest.raises(TypeError):
+        mc.verify_items(d, torch.zeros(4, dtype=torch.int32, device="cuda"))
+
+
+def test_verify_pages_count_only_query(torch):
+    """cap == 0 counts the walk's items and verifies nothing."""
+    import ctypes
+    rng = np.random.default_rng(43)
+    items = [layout.make_item(b"q%05d" % i, rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes(),
+                              cas=i + 1) for i in range(700)]
+    wbuf = 128 << 10
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    mc.stamp_items(buf, offs, region_bytes=wbuf)
+    buf[int(offs[10]) + 60] ^= 4
+    d = _dev(torch, buf)
+    nitems, nbad = ctypes.c_uint64(0), ctypes.c_uint64(7)
+    _lib.check(_lib.lib.crc32c_verify_pages(d.data_ptr(), buf.size, wbuf, None, None, 0, ctypes.byref(nitems),
+                                            ctypes.byref(nbad), _lib.CRC32C_DEVICE, None))
+    assert nitems.value == offs.size and nbad.value == 0
+    got_offs, got_ok, nb = mc.verify_pages(d, wbuf)
+    assert nb == 1 and got_ok.cpu().numpy()[10] == 0
+    np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), offs)
+    # host path: capacity bound from the header
+    got_offs, got_ok, nb = mc.verify_pages(buf, wbuf)
+    assert nb == 1 and got_offs.size == offs.size
