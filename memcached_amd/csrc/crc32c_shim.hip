@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <pthread.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -129,9 +130,18 @@ std::mutex g_dev_mu;
 std::vector<std::unique_ptr<Device>> g_devs;
 int g_ndev = -1;
 
-#define HIP_OK(x)                              \
-    do {                                       \
-        if ((x) != hipSuccess) return CRC32C_EHIP; \
+// MCRC_DEBUG=1 in the environment: report the failing HIP call on stderr.
+bool debug_on() {
+    static const bool on = getenv("MCRC_DEBUG") != nullptr;
+    return on;
+}
+#define HIP_OK(x)                                                                                  \
+    do {                                                                                           \
+        const hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) {                                                                    \
+            if (debug_on()) fprintf(stderr, "mcrc: %s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            return CRC32C_EHIP;                                                                    \
+        }                                                                                          \
     } while (0)
 
 int count_gfx950() {
@@ -289,7 +299,8 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     };
     if (identity) {
         spans(a, grid_for(d, n));
-        return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
+        HIP_OK(hipGetLastError());
+    return CRC32C_OK;
     }
     if (n >= 0xffffffffull) return CRC32C_EINVAL;
     // units fit in cap whenever the spans do not overlap; overlapping long spans
@@ -315,12 +326,13 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     u.span_acc = d.span_acc;
     u.segpow = d.segpow;
     spans(u, d.cus);
-    mcrc_dev::SpanArgs w = a;
+    mcrc_dev::SpanArgs w = u;  // (every table pointer set, even those whole units do not use)
     w.units = d.whole;
     w.nunits = nwhole;
     spans(w, d.cus);
     hipLaunchKernelGGL((mcrc_dev::k_combine<MODE>), dim3(g1), dim3(256), 0, st, u, d.nseg, d.prefix, d.irec, nvalid);
-    return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
+    HIP_OK(hipGetLastError());
+    return CRC32C_OK;
 }
 
 // Enqueue the kernels for a device-resident batch on `st`.
@@ -349,7 +361,8 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
         else
             hipLaunchKernelGGL((K1_KERNEL(false)), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
                                st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1, kfinal, kspan, s.crc_in, s.out);
-        return hipGetLastError() == hipSuccess ? CRC32C_OK : CRC32C_EHIP;
+        HIP_OK(hipGetLastError());
+    return CRC32C_OK;
     }
     mcrc_dev::SpanArgs a{};
     a.base = (const uint8_t *)s.base;
@@ -364,6 +377,7 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
     a.out = s.out;
     a.nbad = d.nbad;  // spans outside the buffer
     a.n = s.n;
+    a.segpow = d.segpow;
     a.xpow = d.xpow;
     a.zero = d.zero;
     HIP_OK(hipMemsetAsync(d.nbad, 0, sizeof(unsigned long long), st));
