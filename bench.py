@@ -337,6 +337,7 @@ def main():
                     choices=["config2", "config2r", "config3", "config5", "pages", "stamp", "host"],
                     help="config2 = headline; others are extra measurements (not the bench line)")
     ap.add_argument("--pages", type=int, default=1000, help="config5: 64 MiB pages per GPU")
+    ap.add_argument("--span-len", type=int, default=4133, help="config2r: span length (stride = len + 32)")
     args = ap.parse_args()
     if args.workload != "config2":
         return extra_workload(args)
@@ -433,17 +434,17 @@ def extra_workload(args):
                    detected_exactly_the_injected_items=exact)
     elif args.workload == "config2r":
         # SURVEY.md 8(d) config 2 variant: realistic 4133-B spans at stride 4165, start +32 (unaligned)
-        n = args.items
+        n, sl = args.items, args.span_len
         g = torch.Generator(device="cuda").manual_seed(42 + rank)
-        data = torch.randint(0, 256, (n * 4165 + 64,), dtype=torch.uint8, device="cuda", generator=g)
+        data = torch.randint(0, 256, (n * (sl + 32) + 64,), dtype=torch.uint8, device="cuda", generator=g)
         out = torch.empty(n, dtype=torch.int32, device="cuda")
-        spans = _lib.Spans(data.data_ptr() + 32, data.numel() - 32, None, 4165, None, 4133, None, out.data_ptr(), n)
+        spans = _lib.Spans(data.data_ptr() + 32, data.numel() - 32, None, sl + 32, None, sl, None, out.data_ptr(), n)
         run_steps(spans, max(1, args.warmup), stream)
         torch.cuda.synchronize()
         elapsed, evs = timed(lambda k: run_steps(spans, k, stream), args.steps, world)
         kms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-        nbytes = n * 4133
-        res.update(config={"workload": f"config 2 variant: {n} x 4133-B spans at stride 4165, start +32 "
+        nbytes = n * sl
+        res.update(config={"workload": f"config 2 variant: {n} x {sl}-B spans at stride {sl + 32}, start +32 "
                                        "(K2, one unit per span)"},
                    kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
                    hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))

@@ -39,10 +39,7 @@ constexpr uint32_t kAuxOp6 = 24;  // M_{128*CH}
 constexpr uint32_t kLdsImage1Bytes = 256 * 64 * 4;              // 64 KiB
 constexpr uint32_t kAux4Bytes = 28 * 1024;                        // 28 KiB
 constexpr uint32_t kLdsImage4Bytes = kAux4Bytes + 2 * 65536;     // 156 KiB
-// Span kernels append 16 rows of 32 dwords: row t, dword i = x^(i - 8t) mod P
-// (the lane-distributed multiply by x^(-8t), crc32c_kernels.hip mul_xinv_group).
-constexpr uint32_t kXinvOffset = kLdsImage4Bytes;
-constexpr uint32_t kLdsSpanBytes = kLdsImage4Bytes + 16 * 32 * 4;  // 158 KiB
+
 constexpr uint32_t kPoly = 0x82f63b78u;
 
 template <int SLICE>
@@ -218,6 +215,22 @@ __device__ __forceinline__ uint32_t group_reduce32_quad(uint32_t ab, uint32_t cd
     v = reduce_level<2>(v, (lane & 7u) < 4u);
     v = reduce_level<3>(v, (lane & 15u) < 4u);
     return reduce_level<4>(v, (lane & 31u) < 4u);
+}
+
+// Span image (crc32c_gf2.h build_lds_image_span): aux tables 16..19 hold the
+// 4 KiB block fold instead of tree level 4.
+constexpr uint32_t kAuxSpanFold = 16;
+
+// group_reduce32_dpp on the span image: level 4 (M_512) is level 3 (M_256)
+// applied twice.
+__device__ __forceinline__ uint32_t group_reduce32_span(uint32_t v, uint32_t lane) {
+    v = reduce_level<0>(v, (lane & 1u) == 0u);
+    v = reduce_level<1>(v, (lane & 3u) == 0u);
+    v = reduce_level<2>(v, (lane & 7u) == 0u);
+    v = reduce_level<3>(v, (lane & 15u) == 0u);
+    const uint32_t x = lane_down<4>(v);
+    if ((lane & 31u) == 0u) v = apply_op<4>(kAuxTree + 12, apply_op<4>(kAuxTree + 12, v)) ^ x;
+    return v;
 }
 
 // Copy a table image from global memory into this workgroup's LDS.

@@ -219,4 +219,17 @@ inline void build_lds_image_k1(uint32_t *img, uint32_t chunk) {
     }
 }
 
+// Span image (160 KiB): the K1 image with aux tables 16..19 (tree level 4,
+// M_{16 chunk}) replaced by the block fold M_{128 chunk} (4 rows of 32 lanes).
+// The span kernels apply level 3 twice for level 4 (once per unit, a few
+// lanes) and fold every 4 KiB block into the lane accumulator with the freed
+// tables; the row folds come from the shifted last-step tables as in K1.
+inline void build_lds_image_span(uint32_t *img, uint32_t chunk) {
+    build_lds_image_k1(img, chunk);
+    uint32_t tabs[4][256];
+    Gf2Op::zeros((uint64_t)chunk * 128).byte_tables(tabs);
+    for (int k = 0; k < 4; ++k)
+        for (uint32_t e = 0; e < 256; ++e) img[(16 + k) * 256 + e] = tabs[k][e];
+}
+
 }  // namespace mcrc

@@ -493,6 +493,7 @@ struct SpanArgs {
                                // MODE 0: spans outside [base, base + base_bytes) (atomic)
     uint64_t n;                // spans (items)
     const uint32_t *xpow;      // x^(8*j), x^(8*1024*j), x^(8*2^20*j) (3 x 1024), x^(-8t) (16)
+    const uint32_t *xinv;      // row t (16 x 32): x^(i - 8t), the lane-distributed multiply by x^(-8t)
     const uint4 *zero;         // kZeroBytes of zeros in device memory
     // work units (nullptr: unit u = span u, one segment)
     const struct UnitRec *units;
@@ -569,16 +570,15 @@ struct UnitDesc {
     const uint8_t *p;  // first byte of this unit
     uint32_t eo;       // e - p: e = 16-aligned end of this unit's grid
     uint32_t Eo;       // E - p: E = end of the span's real bytes (bytes >= E are zeroed)
-    uint32_t niters;   // 4 KiB blocks
-    uint32_t flags;
-    uint32_t raw;      // this lane's dword of the raw record (aux = dword 4, span index = dword 5)
+    uint32_t nf;       // niters << 8 | flags
+    uint32_t raw;      // this lane's dword li & 7 of the unit's raw record: aux (dword 4), span index
+                       // (dword 5) and segment (dword 7) are gathered from it when the unit ends
     static constexpr uint32_t kValid = 1, kSingle = 2, kHead = 4, kSane = 8;
-    __device__ __forceinline__ bool valid() const { return flags & kValid; }
-    __device__ __forceinline__ bool single() const { return flags & kSingle; }
-    __device__ __forceinline__ bool head() const { return flags & kHead; }
-    __device__ __forceinline__ bool sane() const { return flags & kSane; }
-    __device__ __forceinline__ const uint8_t *e() const { return p + eo; }
-    __device__ __forceinline__ const uint8_t *E() const { return p + Eo; }
+    __device__ __forceinline__ uint32_t niters() const { return nf >> 8; }
+    __device__ __forceinline__ bool valid() const { return nf & kValid; }
+    __device__ __forceinline__ bool single() const { return nf & kSingle; }
+    __device__ __forceinline__ bool head() const { return nf & kHead; }
+    __device__ __forceinline__ bool sane() const { return nf & kSane; }
 };
 
 // Unit (segment `seg` of span [base + off, +len), or the whole span) as a record.
@@ -604,44 +604,44 @@ __device__ __forceinline__ UnitRec make_unit(const uint8_t *base, uint64_t off, 
 
 // Raw fetch of unit u.  The record is the same for every lane of a group, so
 // lane j of the group holds only its dword j (one VGPR while the loads are in
-// flight); decode_unit gathers the dwords when the unit is first needed, so the
-// group keeps streaming meanwhile.
+// flight); decode_unit gathers the dwords when the unit is needed.  Nothing
+// here uses the loaded value (a use would make the wave wait for every older
+// load, the block prefetch included): units are fetched two ahead and decoded
+// when their loads are long done.  One-unit-per-span batches (MODE 0, no
+// plan) fetch only the raw span fields: lanes 0/1 the offset, lane 4 crc_in.
 template <int MODE, bool UNITS>
 __device__ __forceinline__ uint32_t fetch_unit(const SpanArgs &a, uint64_t u, uint64_t nunits, uint32_t li) {
     const uint32_t j = li & 7u;
     if (u >= nunits) return 0u;  // flags 0: no unit
     if (UNITS) return reinterpret_cast<const uint32_t *>(a.units + u)[j];
-    // MODE 0, one unit per span: raw item fields {off lo, off hi, len, -, crc_in, u, 1, -}
-    // (selected without branching on the lane: every lane reads the same words)
-    const uint64_t off = a.offsets ? a.offsets[u] : u * a.stride;
-    const uint32_t len = a.lens ? a.lens[u] : a.len;
-    const uint32_t cin = a.crc_in ? a.crc_in[u] : 0u;
-    uint32_t v = j == 0 ? (uint32_t)off : (uint32_t)(off >> 32);
-    v = j == 2 ? len : v;
-    v = j == 4 ? cin : v;
-    v = j == 5 ? (uint32_t)u : v;
-    v = j == 6 ? 1u : v;
-    return (j == 3 || j == 7) ? 0u : v;
+    const uint32_t *src = j < 2u ? (a.offsets ? reinterpret_cast<const uint32_t *>(a.offsets) + 2 * u + j : nullptr)
+                                 : (j == 4u && a.crc_in ? a.crc_in + u : nullptr);
+    return src ? *src : 0u;
 }
 
+// Decode unit u's record (raw: its lane-distributed dwords from fetch_unit).
 template <int MODE, bool UNITS>
-__device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw, uint32_t lane) {
+__device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw, uint64_t u, uint64_t nunits,
+                                                uint32_t lane) {
     const uint32_t g = lane & 32u;
-    UnitRec r;
-    r.a = make_uint4(__shfl(raw, g | 0, 64), __shfl(raw, g | 1, 64), __shfl(raw, g | 2, 64), __shfl(raw, g | 3, 64));
-    r.b = make_uint4(__shfl(raw, g | 4, 64), __shfl(raw, g | 5, 64), __shfl(raw, g | 6, 64), 0u);
-    if (!UNITS && r.b.z) {
-        const uint64_t off = r.a.x | ((uint64_t)r.a.y << 32);
-        const bool sane = off <= a.base_bytes && r.a.z <= a.base_bytes - off;  // else: read nothing
-        r = make_unit(a.base, sane ? off : 0, sane ? r.a.z : 0u, r.b.x, sane, r.b.y, kWhole);
-    }
-    UnitDesc d;  // (aux and the span index stay in raw: read at the unit's end)
-    d.p = a.base + (r.a.x | ((uint64_t)r.a.y << 32));
-    d.eo = r.a.z;
-    d.Eo = r.a.w;
+    UnitDesc d;
     d.raw = raw;
-    d.flags = r.b.z & 0xffu;
-    d.niters = r.b.z >> 8;
+    if (UNITS) {
+        d.p = a.base + ((uint64_t)__shfl(raw, g | 0, 64) | ((uint64_t)__shfl(raw, g | 1, 64) << 32));
+        d.eo = __shfl(raw, g | 2, 64);
+        d.Eo = __shfl(raw, g | 3, 64);
+        d.nf = __shfl(raw, g | 6, 64);
+    } else {
+        // MODE 0, unit = span u: {offset, len, crc_in} -> the unit record
+        const uint64_t off = a.offsets ? (uint64_t)__shfl(raw, g | 0, 64) | ((uint64_t)__shfl(raw, g | 1, 64) << 32)
+                                       : u * a.stride;
+        const bool sane = off <= a.base_bytes && a.len <= a.base_bytes - off;  // else: read nothing
+        const UnitRec r = make_unit(a.base, sane ? off : 0, sane ? a.len : 0u, 0u, sane, 0u, kWhole);
+        d.p = a.base + (r.a.x | ((uint64_t)r.a.y << 32));
+        d.eo = r.a.z;
+        d.Eo = r.a.w;
+        d.nf = u < nunits ? r.b.z : 0u;  // flags 0: no unit
+    }
     return d;
 }
 
@@ -652,22 +652,26 @@ struct BlockWin {
 // Issue the loads of block k of unit d for lane li.
 __device__ __forceinline__ void load_block(BlockWin &w, const UnitDesc &d, uint32_t k, uint32_t li,
                                            const uint4 *zero) {
-    // offsets relative to the unit's first byte p: block start G - p = grel;
-    // piece rel = grel + 1024 r + 32 li + 16 j overlaps [p, E) iff
-    // -16 < rel < Eo, i.e. (uint32)(rel + 15) < Eo + 15.  (A unit with no
-    // bytes has Eo == 0 and reads only zeros.)
-    const int32_t grel = (int32_t)d.eo - (int32_t)(kBlockBytes * (d.niters - k));
+    // Offsets relative to the unit's first byte p: block start G - p = grel;
+    // lane li's row-r chunk is [grel + 1024 r + 32 li, +32), its pieces at +0
+    // and +16.  A piece that ends at or before ph = floor16(p) reads the zero
+    // line (only head blocks have such pieces); every other piece overlaps
+    // [ph, e), so no load leaves the pages of the span.  zl points 16 bytes
+    // into this workgroup's zero line, so zl and zl + 16 are both zeros.
+    const int32_t grel = (int32_t)d.eo - (int32_t)(kBlockBytes * (d.niters() - k));
     const int32_t lrel = grel + (int32_t)(kSpanCH * li);
     const uint8_t *q0 = d.p + lrel;
-    const uint32_t lim = d.Eo + 15u;
+    const uint8_t *zl = reinterpret_cast<const uint8_t *>(zero) + 16;
+    // piece-0 end - ph, row 0; a unit without blocks (no bytes, or no unit)
+    // reads nothing but zeros
+    const int32_t e0 = d.niters() ? lrel + 16 + (int32_t)((uintptr_t)d.p & 15u) : -(int32_t)kBlockBytes - 16;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int32_t off = r * (int32_t)kRowBytes + 16 * j;
-            const bool ok = (uint32_t)(lrel + off + 15) < lim;
-            w.v[r][j] = ld16(ok ? reinterpret_cast<const uint4 *>(q0 + off) : zero);
-        }
+    for (int r = 0; r < 4; ++r) {
+        const uint8_t *rb = q0 + r * kRowBytes;
+        const int32_t er = e0 + r * (int32_t)kRowBytes;
+        w.v[r][0] = ld16(er > 0 ? rb : zl);
+        w.v[r][1] = ld16((er + 16 > 0 ? rb : zl) + 16);
+    }
 }
 
 // Byte masks for dword i of a piece: keep bytes at or after byte k / before byte k.
@@ -690,9 +694,12 @@ __device__ __forceinline__ uint32_t place(uint32_t x, int32_t d) {
     return c == 4 ? 0u : v;                          // (shift 64 would wrap)
 }
 
-// Chains over rows NS..3 of a block, folded to the block's lane value.
+// Chains over rows NS..3 of a block, as in K1: the last step of rows 0-2
+// reads the shifted tables of the span image (row fold included), so the
+// block's lane value is the XOR of the chains.
 template <int NS>
 __device__ __forceinline__ uint32_t block_value(const BlockWin &w, const LaneCtx &c) {
+    constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};
     uint32_t x[4];
 #pragma unroll
     for (int r = NS; r < 4; ++r) x[r] = w.v[r][0].x;
@@ -700,13 +707,16 @@ __device__ __forceinline__ uint32_t block_value(const BlockWin &w, const LaneCtx
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
         for (int r = NS; r < 4; ++r) {
-            const uint32_t wn = i + 1 < 8 ? dw4(w.v[r][(i + 1) >> 2], (i + 1) & 3) : 0u;
-            x[r] = step4_next(x[r], wn, c);
+            if (i + 1 < 8) {
+                x[r] = step4_next(x[r], dw4(w.v[r][(i + 1) >> 2], (i + 1) & 3), c);
+            } else {
+                x[r] = r < 3 ? step4_last_shifted(x[r], kShift[r]) : step4_next(x[r], 0u, c);
+            }
         }
     }
-    uint32_t v = x[NS];
+    uint32_t v = x[3];
 #pragma unroll
-    for (int r = NS + 1; r < 4; ++r) v = apply_op<4>(kAuxOp5, v) ^ x[r];
+    for (int r = NS; r < 3; ++r) v ^= x[r];
     return v;
 }
 
@@ -781,12 +791,13 @@ __device__ __forceinline__ uint32_t mul_row_group(uint32_t v0, const uint32_t *r
     return term;
 }
 
-// v * x^(-8t) mod P spread over a 32-lane group: lane i adds bit i of v (the
-// x^i coefficient) times x^(i-8t) from the LDS table, and the lanes XOR-reduce
-// into lane 0.  v is read from lane 0 of the group; t is per group.
-__device__ __forceinline__ uint32_t mul_xinv_group(uint32_t v0, uint32_t t, uint32_t li) {
+// v * y mod P spread over a 32-lane group: lane i adds bit i of v (the x^i
+// coefficient) times xi = x^i * y (this lane's element of a row of the xinv
+// or segpow table), and the lanes XOR-reduce into lane 0.  v is read from lane
+// 0 of the group.
+__device__ __forceinline__ uint32_t mul_xinv_group(uint32_t v0, uint32_t xi, uint32_t li) {
     const uint32_t v = __shfl(v0, 0, 32);
-    uint32_t term = (v << li) & 0x80000000u ? lds_ld(kXinvOffset + (t << 7) + (li << 2)) : 0u;
+    uint32_t term = (v << li) & 0x80000000u ? xi : 0u;
     term ^= lane_down<0>(term);
     term ^= lane_down<1>(term);
     term ^= lane_down<2>(term);
@@ -807,7 +818,7 @@ constexpr uint32_t kSpanBlock = MCRC_SPAN_BLOCK;
 template <int MODE, bool UNITS>
 __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *__restrict__ img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    load_tables(smem, img, kLdsSpanBytes);
+    load_tables(smem, img, kLdsImageK1Bytes);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t li = lane & 31u;
     LaneCtx c;
@@ -817,8 +828,16 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
     const uint64_t ngroups_total = (uint64_t)gridDim.x * (blockDim.x >> 5);
     uint64_t u = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
 
-    UnitDesc cur = decode_unit<MODE, UNITS>(a, fetch_unit<MODE, UNITS>(a, u, nunits, li), lane);
-    uint32_t nxt = fetch_unit<MODE, UNITS>(a, u + ngroups_total, nunits, li);  // decoded when first needed
+    UnitDesc cur = decode_unit<MODE, UNITS>(a, fetch_unit<MODE, UNITS>(a, u, nunits, li), u, nunits, lane);
+    // Ring of the next four units' raw records, lane-distributed: lanes
+    // 8s..8s+7 of a group hold slot s.  The unit after cur is in slot sl; a
+    // switch decodes it and refills the slot with the unit four further on.
+    // Nothing is copied out of the ring and no load is used right after it is
+    // issued (vmcnt counts in issue order: either would make the wave wait
+    // for the block prefetch too).
+    uint32_t ring = fetch_unit<MODE, UNITS>(a, u + (1 + (li >> 3)) * ngroups_total, nunits, li);
+    const uint32_t *const xinv_rows = a.xinv, *const segpow_rows = a.segpow;
+    uint32_t sl = 0;
     uint32_t k = 0;    // block index inside cur
     uint32_t acc = 0;  // lane accumulator over the blocks of cur
     BlockWin w0, w1;
@@ -832,17 +851,46 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
     // Process the block held in `w` (block k of cur) after issuing the loads of
     // the group's next block into `wn`.  Returns false once this group is done.
     auto step = [&](BlockWin &w, BlockWin &wn) -> bool {
-        const bool last = k + 1 >= cur.niters;
+        const bool last = k + 1 >= cur.niters();
+        // the unit's finishing rows (x^(i - 8t), or the segment shift), loaded
+        // before this step's other loads: the finalisation below waits for
+        // them alone, not for the block prefetch
+        // (loaded unconditionally, from a harmless row when not needed: loads
+        // under divergent branches leave the waitcnt pass a merged state that
+        // drains the prefetch)
+        const uint32_t segk = UNITS ? __shfl(cur.raw, (lane & 32u) | 7u, 64) : 0u;
+        const uint32_t *r1 = cur.single() ? xinv_rows + ((cur.eo - cur.Eo) & 15u) * 32
+                                          : segpow_rows + 32 * (segk & 255u);
+        uint32_t fx1 = 0u;
+        if (__builtin_amdgcn_readfirstlane(__any(last))) fx1 = r1[li];  // (wave-uniform branch)
+        __builtin_amdgcn_sched_barrier(0);  // (issued before the block prefetch, not sunk after it)
+        // next block: block k + 1 of cur, or block 0 of the unit in ring slot sl
         UnitDesc nd;
-        if (!last) {
-            load_block(wn, cur, k + 1, li, zero);
-        } else {
-            nd = decode_unit<MODE, UNITS>(a, nxt, lane);
-            load_block(wn, nd, 0, li, zero);
+        if (__any(last)) {
+            const uint32_t g = lane & 32u, sb = sl << 3;
+            const uint32_t rw = __shfl(ring, g | sb | (li & 7u), 64);  // slot sl, dword li & 7
+            nd = decode_unit<MODE, UNITS>(a, rw, u + ngroups_total, nunits, lane);
         }
-
-        if (cur.niters) {
-            const int32_t grel = (int32_t)cur.eo - (int32_t)(kBlockBytes * (cur.niters - k));  // G - p
+        if (last && (li >> 3) == sl) ring = fetch_unit<MODE, UNITS>(a, u + 5 * ngroups_total, nunits, li);
+        {
+            UnitDesc t = cur;
+            t.p = last ? nd.p : cur.p;
+            t.eo = last ? nd.eo : cur.eo;
+            t.Eo = last ? nd.Eo : cur.Eo;
+            t.nf = last ? nd.nf : cur.nf;
+            load_block(wn, t, last ? 0u : k + 1, li, zero);
+        }
+        // Every path consumes the whole block (a path that skips rows, or a
+        // group without a unit, would otherwise leave the block's loads
+        // pending in the waitcnt pass's view, and the next write to those
+        // registers became an s_waitcnt vmcnt(0) that drained the prefetch).
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                asm volatile("" ::"v"(w.v[r][q].x), "v"(w.v[r][q].y), "v"(w.v[r][q].z), "v"(w.v[r][q].w));
+        if (cur.niters()) {
+            const int32_t grel = (int32_t)cur.eo - (int32_t)(kBlockBytes * (cur.niters() - k));  // G - p
             // head: zero the bytes before p and inject ~crc_in into [p, p+4).
             // Only the lane owning the piece ph that holds p is touched (and,
             // when p & 15 > 12, dword 0 of the next piece, which is in block 1
@@ -881,6 +929,7 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
                             v.z = (v.z & m2) ^ i2;
                             v.w = (v.w & m3) ^ i3;
                         }
+
                         if (sel2 == 2 * r + j) v.x ^= s0;
                     }
             }
@@ -892,12 +941,16 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
             const bool ht = last && li == 31 && te - 1u < 15u;
 #endif
             if (__any(ht)) {
+                // keep the first 16 - te bytes of the piece: two 64-bit masks
                 const uint32_t kt = 16u - te;
+                const uint32_t kl = kt < 8u ? kt : 8u, kq = kt > 8u ? kt - 8u : 0u;
+                const uint64_t ml = kl >= 8u ? ~0ull : (1ull << (8 * kl)) - 1ull;
+                const uint64_t mh = (1ull << (8 * kq)) - 1ull;  // kq < 8
                 uint4 &v = w.v[3][1];
-                v.x = ht ? keep_before(v.x, 0, kt) : v.x;
-                v.y = ht ? keep_before(v.y, 1, kt) : v.y;
-                v.z = ht ? keep_before(v.z, 2, kt) : v.z;
-                v.w = ht ? keep_before(v.w, 3, kt) : v.w;
+                v.x &= ht ? (uint32_t)ml : ~0u;
+                v.y &= ht ? (uint32_t)(ml >> 32) : ~0u;
+                v.z &= ht ? (uint32_t)mh : ~0u;
+                v.w &= ht ? (uint32_t)(mh >> 32) : ~0u;
             }
             // rows wholly before p for every lane of the wave are skipped
             // (a group without a unit has niters == 0 and votes to skip)
@@ -912,28 +965,35 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
                 case 2: v = block_value<2>(w, c); break;
                 default: v = block_value<3>(w, c); break;
             }
-            acc = apply_op<4>(kAuxOp6, acc) ^ v;
+            acc = apply_op<4>(kAuxSpanFold, acc) ^ v;
         }
         if (last) {
             if (cur.valid()) {
-                uint32_t raw = group_reduce32_dpp(acc, lane);
+#ifdef MCRC_ABL_NOTREE  // ablation: no lane-group tree (wrong CRCs)
+                uint32_t raw = acc;
+#else
+                uint32_t raw = group_reduce32_span(acc, lane);
+#endif
                 if (cur.single()) {
                     const uint32_t t = cur.eo - cur.Eo;  // tail padding
                     const uint32_t aux = __shfl(cur.raw, (lane & 32u) | 4u, 64);
-                    const uint32_t item = __shfl(cur.raw, (lane & 32u) | 5u, 64);
+                    const uint32_t item = UNITS ? __shfl(cur.raw, (lane & 32u) | 5u, 64) : (uint32_t)u;
+#ifndef MCRC_ABL_NOSHORT
                     if (li == 0 && cur.Eo < 4) raw ^= short_init<MODE>(a, aux, cur.Eo, t);
+#endif
 #ifdef MCRC_ABL_NOFIN  // ablation: no x^-8t multiply (wrong CRCs)
                     const uint32_t v = raw ^ t;
 #else
-                    const uint32_t v = mul_xinv_group(raw, t, li);
+                    const uint32_t v = mul_xinv_group(raw, fx1, li);
 #endif
                     if (li == 0) emit<MODE>(a, item, ~v, aux, cur.sane(), cur.p);
                 } else {
                     // segment s of nseg: raw_v(span) gets M_{64Ki * (nseg-1-s)}(raw)
-                    const uint32_t k = __shfl(cur.raw, (lane & 32u) | 7u, 64);
                     const uint32_t item = __shfl(cur.raw, (lane & 32u) | 5u, 64);
-                    uint32_t v = mul_row_group(raw, a.segpow + 32 * (k & 255u), li);
-                    v = mul_row_group(v, a.segpow + 32 * (256 + (k >> 8)), li);
+                    // (the second factor, for spans past 16 MiB only, is loaded here: one
+                    // register fewer across the step, a drain only at such segment ends)
+                    uint32_t v = mul_xinv_group(raw, fx1, li);
+                    if (__any(segk >= 256u)) v = mul_xinv_group(v, segpow_rows[32 * (256 + (segk >> 8)) + li], li);
                     if (li == 0) atomicXor(a.span_acc + item, v);
                 }
             }
@@ -941,16 +1001,24 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
             k = 0;
             u += ngroups_total;
             cur = nd;
-            nxt = fetch_unit<MODE, UNITS>(a, u + ngroups_total, nunits, li);
+            sl = (sl + 1u) & 3u;
         } else {
             ++k;
         }
         return cur.valid();
     };
 
+    // nothing issued before the loop stays pending into it (the waitcnt pass
+    // would otherwise wait for it, vmcnt(0), at the top of every iteration)
+    __builtin_amdgcn_s_waitcnt(0);
+    // One, wave-uniform exit at the bottom (a group that has finished runs
+    // empty steps until the other has): a divergent or mid-loop exit gives the
+    // loop header an un-waited predecessor, and the waitcnt pass then drains
+    // the prefetch there (vmcnt(0)) on every iteration.
     for (;;) {
-        if (!step(w0, w1)) break;
-        if (!step(w1, w0)) break;
+        step(w0, w1);
+        step(w1, w0);
+        if (!__builtin_amdgcn_readfirstlane(__any(cur.valid()))) break;
     }
 }
 

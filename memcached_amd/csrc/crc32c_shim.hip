@@ -66,7 +66,8 @@ struct Device {
     int id = -1;
     int cus = 0;
     bool ok = false;
-    uint4 *img = nullptr;       // LDS table image (CH = 32) for every kernel
+    uint4 *img = nullptr;       // LDS table image of the span kernels (crc32c_gf2.h build_lds_image_span)
+    uint32_t *xinv = nullptr;   // 16 rows x^(i - 8t), i < 32: x^(-8t) spread over a lane group
     uint4 *img_k1 = nullptr;    // K1 image (160 KiB, crc32c_gf2.h build_lds_image_k1)
     uint32_t *xpow = nullptr;   // 3 x 1024 x^(8n) table
     uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
@@ -162,12 +163,12 @@ int init_device(Device &d, int id) {
     HIP_OK(hipGetDeviceProperties(&p, id));
     if (strncmp(p.gcnArchName, "gfx950", 6) != 0) return CRC32C_ENODEV;
     d.cus = p.multiProcessorCount;
-    std::vector<uint32_t> img(mcrc_dev::kLdsSpanBytes / 4);
-    mcrc::build_lds_image4(img.data(), mcrc_dev::kSpanCH);
+    std::vector<uint32_t> img(mcrc::kImageK1Dwords);
+    mcrc::build_lds_image_span(img.data(), mcrc_dev::kSpanCH);
+    std::vector<uint32_t> xinv(16 * 32);
     for (uint32_t t = 0; t < 16; ++t) {  // x^(i - 8t): lane-distributed multiply by x^(-8t)
-        const uint32_t xinv = mcrc::xpow8n_inv(t);
-        for (uint32_t i = 0; i < 32; ++i)
-            img[mcrc_dev::kXinvOffset / 4 + t * 32 + i] = mcrc::mulmodp(0x80000000u >> i, xinv);
+        const uint32_t xi = mcrc::xpow8n_inv(t);
+        for (uint32_t i = 0; i < 32; ++i) xinv[t * 32 + i] = mcrc::mulmodp(0x80000000u >> i, xi);
     }
     std::vector<uint32_t> xp(3 * 1024 + 16);
     for (uint32_t j = 0; j < 1024; ++j) {
@@ -178,6 +179,8 @@ int init_device(Device &d, int id) {
     for (uint32_t t = 0; t < 16; ++t) xp[3072 + t] = mcrc::xpow8n_inv(t);
     HIP_OK(hipMalloc(&d.img, img.size() * 4));
     HIP_OK(hipMemcpy(d.img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMalloc(&d.xinv, xinv.size() * 4));
+    HIP_OK(hipMemcpy(d.xinv, xinv.data(), xinv.size() * 4, hipMemcpyHostToDevice));
     std::vector<uint32_t> img_k1(mcrc::kImageK1Dwords);
     mcrc::build_lds_image_k1(img_k1.data(), kFixedCH);
     HIP_OK(hipMalloc(&d.img_k1, img_k1.size() * 4));
@@ -218,7 +221,7 @@ int init_device(Device &d, int id) {
         (const void *)mcrc_dev::k_spans<2, true>,
     };
     for (const void *k : spans)
-        HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsSpanBytes));
+        HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImageK1Bytes));
     d.ok = true;
     return CRC32C_OK;
 }
@@ -292,10 +295,10 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     auto spans = [&](const mcrc_dev::SpanArgs &x, int grid) {
         if (x.units)
             hipLaunchKernelGGL((mcrc_dev::k_spans<MODE, true>), dim3(grid), dim3(mcrc_dev::kSpanBlock),
-                               mcrc_dev::kLdsSpanBytes, st, x, d.img);
+                               mcrc_dev::kLdsImageK1Bytes, st, x, d.img);
         else
             hipLaunchKernelGGL((mcrc_dev::k_spans<MODE, false>), dim3(grid), dim3(mcrc_dev::kSpanBlock),
-                               mcrc_dev::kLdsSpanBytes, st, x, d.img);
+                               mcrc_dev::kLdsImageK1Bytes, st, x, d.img);
     };
     if (identity) {
         spans(a, grid_for(d, n));
@@ -379,6 +382,7 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
     a.n = s.n;
     a.segpow = d.segpow;
     a.xpow = d.xpow;
+    a.xinv = d.xinv;
     a.zero = d.zero;
     HIP_OK(hipMemsetAsync(d.nbad, 0, sizeof(unsigned long long), st));
     const bool aligned = (flags & CRC32C_ALIGNED16) ||
@@ -611,6 +615,7 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
     a.nbad = d->nbad;
     a.n = n;
     a.xpow = d->xpow;
+    a.xinv = d->xinv;
     a.zero = d->zero;
     a.region = region_bytes;
     d->acquire(st);
@@ -866,6 +871,7 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     a.nbad = d->nbad;
     a.n = total;
     a.xpow = d->xpow;
+    a.xinv = d->xinv;
     a.zero = d->zero;
     a.region = wbuf_bytes;
     HIP_OK(hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st));

@@ -2,7 +2,7 @@
 import glob, json, os, sys, collections
 rows = collections.defaultdict(list)
 for p in sorted(glob.glob(os.path.join(sys.argv[1], "*.json"))):
-    name = os.path.basename(p)[:-5].rsplit("_", 1)[0]
+    name = os.path.basename(p)[:-5].rsplit("_", 1)[0] if p.endswith(("_1.json", "_2.json", "_3.json")) else os.path.basename(p)[:-5]
     try:
         d = json.load(open(p))
         rows[name].append(f"{d['kernel_ms']:.3f}ms/{d['hbm_frac']:.3f}")

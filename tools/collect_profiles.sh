@@ -6,6 +6,7 @@ O=gpurun_out/$R
 P=profiles
 cp $O/pytest_gpu.log $P/${R}_pytest_gpu.log
 cp $O/bench.json $P/${R}_bench.json
+[ -f $O/bench_default.json ] && cp $O/bench_default.json $P/${R}_bench_default.json
 cp $O/kt/kt_kernel_stats.csv $P/${R}_bench_kernel_stats.csv
 cp $O/traffic.json $P/${R}_traffic.json
 cp $O/kt_c3/c3_kernel_stats.csv $P/${R}_config3_kernel_stats.csv
