@@ -453,11 +453,16 @@ def extra_workload(args):
         base, size, region, offs, n, okp = vargs
         nitems, nbad = ctypes.c_uint64(0), ctypes.c_uint64(0)
         sptr = ctypes.c_void_p(stream.cuda_stream)
+        # walk outputs: at most one item more per wbuf than were written
+        cap = n + size // region + 1
+        woffs = torch.empty(cap, dtype=torch.int64, device="cuda")
+        wok = torch.empty(cap, dtype=torch.uint8, device="cuda")
 
         def one():
             if args.workload == "pages":  # device walk + verify (storage.c:950-1070)
-                _lib.check(_lib.lib.crc32c_verify_pages(base, size, region, None, None, 0, ctypes.byref(nitems),
-                                                        ctypes.byref(nbad), _lib.CRC32C_DEVICE, sptr))
+                _lib.check(_lib.lib.crc32c_verify_pages(base, size, region, woffs.data_ptr(), wok.data_ptr(), cap,
+                                                        ctypes.byref(nitems), ctypes.byref(nbad),
+                                                        _lib.CRC32C_DEVICE, sptr))
             else:  # spill CRCs stamped into every image (storage.c:567 per wbuf)
                 _lib.check(_lib.lib.crc32c_stamp_items(base, size, region, offs, n, None, ctypes.byref(nbad),
                                                        _lib.CRC32C_DEVICE, sptr))
