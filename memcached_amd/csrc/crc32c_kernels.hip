@@ -4,15 +4,15 @@
 //     stride, len = R*LPI*CH (extstore spill batches of one slab class;
 //     BASELINE configs 2 and 4).  Replaces N calls of crc32c(0, item, len),
 //     crc32c_hw (crc32c.c:161-246) reached from storage.c:567.
-// K2  k_spans<MODE=0, UNITS>: any offsets, lengths and alignment; one 32-lane
-//     group per work unit of <= 64 KiB (configs 3 and 5, storage.c:172
-//     read-back spans).
-// K3  k_spans<MODE=1>: verify packed item images in extstore pages: the
-//     span [off+32, off+ITEM_ntotal) is checked against the CRC stored in the
-//     item's exptime field (storage.c:160-178 over the page walk of
-//     storage.c:950-960).
-//     k_spans<MODE=2>: stamp: the same spans, the CRC written into exptime
-//     (the spill CRC of storage.c:567, batched per wbuf).
+// K2  k_spans<UNITS>: any offsets, lengths and alignment; one 32-lane group
+//     per work unit of <= 64 KiB (configs 3 and 5, storage.c:172 read-back
+//     spans), then k_final<MODE 0> per span.
+// K3  the same kernel over the spans of packed item images in extstore pages,
+//     [off+32, off+ITEM_ntotal) (k_count<MODE 1/2> parses the headers):
+//     k_final<MODE 1> checks the CRC stored in the item's exptime field
+//     (storage.c:160-178 over the page walk of storage.c:950-960);
+//     k_final<MODE 2> stamps it (the spill CRC of storage.c:567, batched per
+//     wbuf).
 //
 // See crc32c_device.h for the lane-group work model and LDS table layouts.
 #include "crc32c_device.h"
@@ -434,13 +434,17 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 // K2/K3: arbitrary spans, one 32-lane group per work unit
 // ===========================================================================
 //
-// Virtual span.  A span [p, E) is processed as [p, Ea) with Ea = E rounded up
-// to 16: the t = Ea - E bytes after E are zeroed, so the kernel computes
-// raw_v = M_t(raw(D')) and the finalisation multiplies by x^(-8t).  D' is D
-// with ~crc_in XORed into its first four bytes -- exactly what a CRC register
-// initialised to ~crc_in does to them (crc32c.c:166, :397) -- so for
-// |D| >= 4:   crc32c(crc_in, D) = ~M_{-t}(raw_v).
-// Every load is a 16-B aligned piece, and bytes before p are zero.
+// Pieces as they lie.  A span D = [p, E) is read as the 16-B aligned pieces
+// [ph, Ea), ph = p rounded down and Ea = E rounded up to 16, foreign bytes
+// included: the span kernel computes R = raw([ph, Ea)) with no masking and no
+// initial value.  With F_h = [ph, p), F_t = [E, Ea), t = |F_t|, the algebra of
+// crc32c.c:58-137 gives
+//   raw([ph, Ea)) = M_{|D|+t}(raw(F_h)) ^ M_t(raw(D)) ^ raw(F_t), so
+//   crc32c(c, D) = ~M_{-t}(R ^ Z),   Z = M_{|D|+t}(~c ^ raw(F_h)) ^ raw(F_t).
+// Z depends only on c and the at most 30 foreign bytes, so one thread per
+// span computes it (span_corr: k_count before the span kernel, or k_final
+// after it), at a thirty-second of the cost of doing it in a 32-lane group;
+// the span kernel's per-unit work is its lane reduction and one store.
 //
 // Work units.  A virtual span longer than kSegBytes is cut into segments of
 // kSegBytes anchored at Ea (segment 0, the head, holds the remainder: 17 B to
@@ -448,8 +452,10 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 // more than 64 KiB and a batch of
 // Zipf-sized items balances over the grid.  Units come from k_count ->
 // exclusive scan -> k_expand; a batch whose spans all fit one unit uses unit
-// u = span u directly.  k_combine folds the segment values of long spans:
-//   raw_v(span) = sum_s M_{64 KiB * (nseg-1-s)}(raw_v(segment s))   (Horner)
+// u = span u directly.  Segment units shift their value into place and XOR it
+// into the span's accumulator:
+//   R(span) = sum_s M_{64 KiB * (nseg-1-s)}(R(segment s)),
+// then k_final turns R into the CRC (or the verdict) of every span.
 //
 // Unit geometry (the K1 geometry: CH = 32, LPI = 32): a unit [p, e), e
 // 16-aligned, is covered by `niters` blocks of 4 KiB anchored at e; block k
@@ -462,9 +468,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 //
 // Loads are 16-B aligned pieces that overlap [p, E) (so they never leave the
 // pages holding the span); a piece wholly outside is read from a zeroed device
-// buffer instead, so no load is predicated.  Only two pieces per span hold
-// foreign bytes: the one containing p (masked in the head block) and the last
-// one (bytes >= E; lane 31 / row 3 / piece 1 of the last block).
+// buffer instead, so no load is predicated.
 
 constexpr uint32_t kSpanCH = 32;
 constexpr uint32_t kRowBytes = 32 * kSpanCH;  // 1024
@@ -485,20 +489,20 @@ struct SpanArgs {
     uint64_t stride;           // when offsets == nullptr: base + i * stride
     const uint32_t *lens;      // per-span lengths, or nullptr: every span is `len`
     uint32_t len;
-    uint32_t kspan16[16];      // lens == nullptr: x^(8*(len+t)) for t = 0..15
     const uint32_t *crc_in;    // MODE 0: per-span initial CRC or nullptr (0)
     uint32_t *out;             // MODE 0: CRC per span
     uint8_t *ok;               // MODE 1: 1 if the stored CRC matches
     unsigned long long *nbad;  // MODE 1/2: count of mismatches / malformed images;
                                // MODE 0: spans outside [base, base + base_bytes) (atomic)
     uint64_t n;                // spans (items)
-    const uint32_t *xpow;      // x^(8*j), x^(8*1024*j), x^(8*2^20*j) (3 x 1024), x^(-8t) (16)
-    const uint32_t *xinv;      // row t (16 x 32): x^(i - 8t), the lane-distributed multiply by x^(-8t)
+    const uint32_t *xpow;      // x^(8*j), x^(8*1024*j), x^(8*2^20*j) (3 x 1024), x^(-8t) (16),
+                               // x^(8*2^30*j) (8): layout kXpow*
+    const uint32_t *tab8;      // byte-wise table (crc32c_table_little[0], crc32c.c:399), 256 entries
     const uint4 *zero;         // kZeroBytes of zeros in device memory
     // work units (nullptr: unit u = span u, one segment)
     const struct UnitRec *units;
     const uint32_t *nunits;    // device-side unit count
-    uint32_t *span_acc;        // multi-segment spans: XOR of the shifted segment values
+    uint32_t *span_acc;        // planned batches: R per span (segment units XOR their shifted values in)
     const uint32_t *segpow;    // rows k (x^i * x^(8 * 64Ki * k), i < 32) for k < 256, then k = 256 j
     uint64_t region;           // MODE 1: items never cross a multiple of `region` (0: no bound)
 };
@@ -519,10 +523,80 @@ __device__ __forceinline__ uint32_t tail_pad(const uint8_t *p, uint32_t len) {
     return (uint32_t)(-(uintptr_t)(p + len)) & 15u;
 }
 
-// Segments of a virtual span of vlen bytes.  The head segment keeps more than
-// 16 bytes (up to kSegBytes + 16), so the injected ~crc_in never leaves it.
+// Segments of a virtual span of vlen bytes, anchored at Ea; the head segment
+// keeps the remainder (17 B up to kSegBytes + 16 B).
 __device__ __forceinline__ uint32_t nseg_of(uint32_t vlen) {
     return vlen <= kSegBytes + 16 ? 1u : (vlen - 16 + kSegBytes - 1) / kSegBytes;
+}
+
+// Layout of the x^(8n) table (SpanArgs::xpow).
+constexpr uint32_t kXpowInv = 3072;  // x^(-8t), t < 16
+constexpr uint32_t kXpowL3 = 3088;   // x^(8 * 2^30 * j), j < 8
+constexpr uint32_t kXpowDwords = kXpowL3 + 8;
+
+// x^(8n) mod P (n < 2^33): one to four table entries multiplied.
+__device__ __forceinline__ uint32_t xpow8_dev(const uint32_t *xp, uint64_t n) {
+    uint32_t r = xp[n & 1023u];
+    if (n >> 10) r = mulmodp_dev(r, xp[1024 + ((n >> 10) & 1023u)]);
+    if (n >> 20) r = mulmodp_dev(r, xp[2048 + ((n >> 20) & 1023u)]);
+    if (n >> 30) r = mulmodp_dev(r, xp[kXpowL3 + (uint32_t)(n >> 30)]);
+    return r;
+}
+
+// A 16-B piece as two little-endian halves.
+struct Piece {
+    uint64_t lo, hi;
+};
+__device__ __forceinline__ Piece ld_piece(const uint8_t *p) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(p);
+    return {v.x | ((uint64_t)v.y << 32), v.z | ((uint64_t)v.w << 32)};
+}
+// Bytes moved s positions up (s <= 16), zeros shifted in.
+__device__ __forceinline__ Piece shl_bytes(Piece v, uint32_t s) {
+    if (s >= 16) return {0, 0};
+    if (s >= 8) return {0, v.lo << (8 * (s - 8))};
+    if (s == 0) return v;
+    return {v.lo << (8 * s), (v.hi << (8 * s)) | (v.lo >> (64 - 8 * s))};
+}
+// Register after the 16 bytes of v from a zero register (the byte-wise loop
+// of crc32c.c:399, t8 = its table crc32c_table_little[0]).
+__device__ __forceinline__ uint32_t raw16(Piece v, const uint32_t *t8) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        r ^= (uint32_t)((k < 2 ? v.lo : v.hi) >> (32 * (k & 1)));
+#pragma unroll
+        for (int b = 0; b < 4; ++b) r = t8[r & 255u] ^ (r >> 8);
+    }
+    return r;
+}
+
+// Z of span [p, p + len) with initial CRC c (see "Pieces as they lie"):
+//   crc32c(c, D) = ~M_{-t}(R ^ Z),  Z = M_{len+t}(~c ^ raw(F_h)) ^ raw(F_t).
+// raw(F_h) = raw of the head piece's first kh bytes moved to its top (leading
+// zeros leave a zero register unchanged); raw(F_t) = raw of the tail piece
+// with its first 16 - t bytes cleared.  A span without bytes is not read by
+// the span kernel (R = 0): Z = M_t(~c).  One thread; t8 in LDS.
+__device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, uint32_t c, const uint32_t *t8,
+                                              const uint32_t *xp) {
+    const uint32_t t = tail_pad(p, len);
+    if (len == 0) return mulmodp_dev(~c, xp[t]);
+    const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
+    uint32_t y = ~c;
+    if (kh) y ^= raw16(shl_bytes(ld_piece(p - kh), 16 - kh), t8);
+    uint32_t z = mulmodp_dev(y, xpow8_dev(xp, (uint64_t)len + t));
+    if (t) {
+        const Piece v = ld_piece(p + len + t - 16);
+        const Piece m = shl_bytes({~0ull, ~0ull}, 16 - t);
+        z ^= raw16({v.lo & m.lo, v.hi & m.hi}, t8);
+    }
+    return z;
+}
+
+// The byte table into LDS (k_count, k_final: 256-thread blocks).
+__device__ __forceinline__ void load_tab8(uint32_t *s8, const uint32_t *tab8) {
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s8[i] = tab8[i];
+    __syncthreads();
 }
 
 template <int MODE>
@@ -557,22 +631,23 @@ __device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
 
 // Work-unit record written by k_expand (32 B, one dwordx4 pair per unit):
 //   a = {offset of the unit's first byte from base (lo, hi), e - p, E - p}
-//   b = {aux, span index, flags | niters << 8, nseg - 1 - segment}
+//   b = {z (the span's item record), span index, flags | niters << 8, nseg - 1 - segment}
 struct alignas(16) UnitRec {
     uint4 a, b;
 };
 
-// Item record written by k_count: {offset of the span (lo, hi | !sane << 31), len, aux}.
+// Item record written by k_count: {offset of the span (lo, hi | !sane << 31), len, z}:
+// z = Z (span_corr; MODE 0 and 2) or, for a verify (MODE 1), W = Z ^ M_t(~stored CRC),
+// so that the stored CRC matches iff R == W.
 constexpr uint32_t kInsane = 0x80000000u;
 
 // Decoded descriptor of one work unit (two are live per lane).
 struct UnitDesc {
     const uint8_t *p;  // first byte of this unit
     uint32_t eo;       // e - p: e = 16-aligned end of this unit's grid
-    uint32_t Eo;       // E - p: E = end of the span's real bytes (bytes >= E are zeroed)
     uint32_t nf;       // niters << 8 | flags
-    uint32_t raw;      // this lane's dword li & 7 of the unit's raw record: aux (dword 4), span index
-                       // (dword 5) and segment (dword 7) are gathered from it when the unit ends
+    uint32_t raw;      // this lane's dword li & 7 of the unit's raw record: span index (dword 5)
+                       // and segment (dword 7) are gathered from it when the unit ends
     static constexpr uint32_t kValid = 1, kSingle = 2, kHead = 4, kSane = 8;
     __device__ __forceinline__ uint32_t niters() const { return nf >> 8; }
     __device__ __forceinline__ bool valid() const { return nf & kValid; }
@@ -607,20 +682,19 @@ __device__ __forceinline__ UnitRec make_unit(const uint8_t *base, uint64_t off, 
 // flight); decode_unit gathers the dwords when the unit is needed.  Nothing
 // here uses the loaded value (a use would make the wave wait for every older
 // load, the block prefetch included): units are fetched two ahead and decoded
-// when their loads are long done.  One-unit-per-span batches (MODE 0, no
-// plan) fetch only the raw span fields: lanes 0/1 the offset, lane 4 crc_in.
-template <int MODE, bool UNITS>
+// when their loads are long done.  One-unit-per-span batches (no plan) fetch
+// only the span's offset (lanes 0/1).
+template <bool UNITS>
 __device__ __forceinline__ uint32_t fetch_unit(const SpanArgs &a, uint64_t u, uint64_t nunits, uint32_t li) {
     const uint32_t j = li & 7u;
     if (u >= nunits) return 0u;  // flags 0: no unit
     if (UNITS) return reinterpret_cast<const uint32_t *>(a.units + u)[j];
-    const uint32_t *src = j < 2u ? (a.offsets ? reinterpret_cast<const uint32_t *>(a.offsets) + 2 * u + j : nullptr)
-                                 : (j == 4u && a.crc_in ? a.crc_in + u : nullptr);
+    const uint32_t *src = j < 2u && a.offsets ? reinterpret_cast<const uint32_t *>(a.offsets) + 2 * u + j : nullptr;
     return src ? *src : 0u;
 }
 
 // Decode unit u's record (raw: its lane-distributed dwords from fetch_unit).
-template <int MODE, bool UNITS>
+template <bool UNITS>
 __device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw, uint64_t u, uint64_t nunits,
                                                 uint32_t lane) {
     const uint32_t g = lane & 32u;
@@ -629,17 +703,15 @@ __device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw,
     if (UNITS) {
         d.p = a.base + ((uint64_t)__shfl(raw, g | 0, 64) | ((uint64_t)__shfl(raw, g | 1, 64) << 32));
         d.eo = __shfl(raw, g | 2, 64);
-        d.Eo = __shfl(raw, g | 3, 64);
         d.nf = __shfl(raw, g | 6, 64);
     } else {
-        // MODE 0, unit = span u: {offset, len, crc_in} -> the unit record
+        // unit = span u: {offset, len} -> the unit record
         const uint64_t off = a.offsets ? (uint64_t)__shfl(raw, g | 0, 64) | ((uint64_t)__shfl(raw, g | 1, 64) << 32)
                                        : u * a.stride;
         const bool sane = off <= a.base_bytes && a.len <= a.base_bytes - off;  // else: read nothing
         const UnitRec r = make_unit(a.base, sane ? off : 0, sane ? a.len : 0u, 0u, sane, 0u, kWhole);
         d.p = a.base + (r.a.x | ((uint64_t)r.a.y << 32));
         d.eo = r.a.z;
-        d.Eo = r.a.w;
         d.nf = u < nunits ? r.b.z : 0u;  // flags 0: no unit
     }
     return d;
@@ -674,26 +746,6 @@ __device__ __forceinline__ void load_block(BlockWin &w, const UnitDesc &d, uint3
     }
 }
 
-// Byte masks for dword i of a piece: keep bytes at or after byte k / before byte k.
-__device__ __forceinline__ uint32_t keep_from(uint32_t v, int32_t i, uint32_t k) {
-    int32_t z = (int32_t)k - 4 * i;
-    z = z < 0 ? 0 : z > 4 ? 4 : z;
-    return v & (uint32_t)(0xffffffffull << (8 * z));
-}
-__device__ __forceinline__ uint32_t keep_before(uint32_t v, int32_t i, uint32_t k) {
-    int32_t z = (int32_t)k - 4 * i;
-    z = z < 0 ? 0 : z > 4 ? 4 : z;
-    return v & (uint32_t)((1ull << (8 * z)) - 1ull);
-}
-// Bytes of the 4-byte value x placed at byte offset -d relative to a dword
-// (d = dword position - position of x, in bytes; |d| >= 4 gives 0).
-__device__ __forceinline__ uint32_t place(uint32_t x, int32_t d) {
-    const int32_t c = d < -4 ? -4 : d > 4 ? 4 : d;  // v_med3
-    const uint64_t wide = (uint64_t)x << 32;         // x at bytes 4..7
-    const uint32_t v = (uint32_t)(wide >> (32 + 8 * c));
-    return c == 4 ? 0u : v;                          // (shift 64 would wrap)
-}
-
 // Chains over rows NS..3 of a block, as in K1: the last step of rows 0-2
 // reads the shifted tables of the span image (row fold included), so the
 // block's lane value is the XOR of the chains.
@@ -720,30 +772,16 @@ __device__ __forceinline__ uint32_t block_value(const BlockWin &w, const LaneCtx
     return v;
 }
 
-// x^(8*len) mod P from the three-level table (len < 2^30).
-__device__ __forceinline__ uint32_t xpow8_dev(const uint32_t *xp, uint32_t len) {
-    uint32_t r = xp[len & 1023u];
-    if (len >> 10) r = mulmodp_dev(r, xp[1024 + ((len >> 10) & 1023u)]);
-    if (len >> 20) r = mulmodp_dev(r, xp[2048 + ((len >> 20) & 1023u)]);
-    return r;
-}
-
-// Store (MODE 0), compare (MODE 1) or stamp (MODE 2) the final CRC of span
-// `item`, which starts at p.  Stamp writes the spill CRC into the image's
-// exptime field, bytes 28..31 = p - 4 (storage.c:567), or into out[] when the
-// caller stages the images (host path); ok[] (if any) marks stamped images.
+// Store (MODE 0) or stamp (MODE 2) the CRC of span `item`, which starts at p.
+// Stamp writes the spill CRC into the image's exptime field, bytes 28..31 =
+// p - 4 (storage.c:567), or into out[] when the caller stages the images (host
+// path); ok[] (if any) marks stamped images.  A span that is not sane (outside
+// the buffer, or a malformed image) was not read: counted in nbad.
 template <int MODE>
-__device__ __forceinline__ void emit(const SpanArgs &a, uint64_t item, uint32_t crc, uint32_t aux, bool sane,
-                                     const uint8_t *p) {
+__device__ __forceinline__ void emit(const SpanArgs &a, uint64_t item, uint32_t crc, bool sane, const uint8_t *p) {
     if (MODE == 0) {
         a.out[item] = sane ? crc : 0u;
-        if (!sane) atomicAdd(a.nbad, 1ull);  // span outside the buffer: not read
-    } else if (MODE == 1) {
-        const bool good = sane && crc == aux;
-        a.ok[item] = good;
-#ifndef MCRC_ABL_NOHEAD  // (the ablation's CRCs are wrong: do not count them)
-        if (!good) atomicAdd(a.nbad, 1ull);
-#endif
+        if (!sane) atomicAdd(a.nbad, 1ull);
     } else {
         if (a.ok) a.ok[item] = sane;
         if (!sane) {
@@ -760,42 +798,11 @@ __device__ __forceinline__ void emit(const SpanArgs &a, uint64_t item, uint32_t 
     }
 }
 
-// M_{len+t}(~crc_in) for a span too short (< 4 B) to carry the injected ~crc_in.
-template <int MODE>
-__device__ __forceinline__ uint32_t short_init(const SpanArgs &a, uint32_t aux, uint32_t len, uint32_t t) {
-    const uint32_t xl = (MODE == 0 && a.lens == nullptr) ? a.kspan16[t] : xpow8_dev(a.xpow, len + t);
-    return mulmodp_dev(MODE == 0 ? ~aux : 0xffffffffu, xl);
-}
-
-// crc32c(c, D) from raw_v (one thread; k_combine).
-template <int MODE>
-__device__ __forceinline__ void finalize(const SpanArgs &a, uint64_t item, uint32_t raw_v, uint32_t aux,
-                                         const uint8_t *p, uint32_t span_len, bool sane) {
-    const uint32_t t = tail_pad(p, span_len);
-    uint32_t v = raw_v;
-    if (span_len < 4) v ^= short_init<MODE>(a, aux, span_len, t);
-    if (t) v = mulmodp_dev(v, a.xpow[3072 + t]);
-    emit<MODE>(a, item, ~v, aux, sane, p);
-}
-
-// v0 (lane 0 of the group) times the element whose row `row` holds
-// x^i * element (i < 32) in global memory; the product lands in lane 0.
-__device__ __forceinline__ uint32_t mul_row_group(uint32_t v0, const uint32_t *row, uint32_t li) {
-    const uint32_t v = __shfl(v0, 0, 32);
-    uint32_t term = (v << li) & 0x80000000u ? row[li] : 0u;
-    term ^= lane_down<0>(term);
-    term ^= lane_down<1>(term);
-    term ^= lane_down<2>(term);
-    term ^= lane_down<3>(term);
-    term ^= lane_down<4>(term);
-    return term;
-}
-
 // v * y mod P spread over a 32-lane group: lane i adds bit i of v (the x^i
-// coefficient) times xi = x^i * y (this lane's element of a row of the xinv
-// or segpow table), and the lanes XOR-reduce into lane 0.  v is read from lane
-// 0 of the group.
-__device__ __forceinline__ uint32_t mul_xinv_group(uint32_t v0, uint32_t xi, uint32_t li) {
+// coefficient) times xi = x^i * y (this lane's element of a row of the segpow
+// table), and the lanes XOR-reduce into lane 0.  v is read from lane 0 of the
+// group.
+__device__ __forceinline__ uint32_t mul_row_group(uint32_t v0, uint32_t xi, uint32_t li) {
     const uint32_t v = __shfl(v0, 0, 32);
     uint32_t term = (v << li) & 0x80000000u ? xi : 0u;
     term ^= lane_down<0>(term);
@@ -809,13 +816,16 @@ __device__ __forceinline__ uint32_t mul_xinv_group(uint32_t v0, uint32_t xi, uin
 #ifndef MCRC_SPAN_BLOCK
 #define MCRC_SPAN_BLOCK 1024
 #endif
-// 16 waves per CU (128 VGPRs).  768 threads (168 VGPRs) removes the few
-// remaining spills but measured slower (config 3: 5.99 vs 5.90 ms; config 5:
-// 6.90 vs 5.93 ms per 300 pages): latency hiding of the dependent lookup
-// chains needs the waves more than the spilled registers cost.
+// 16 waves per CU (128 VGPRs).  768 threads (168 VGPRs) measured slower
+// (config 3: 5.99 vs 5.90 ms; config 5: 6.90 vs 5.93 ms per 300 pages):
+// latency hiding of the dependent lookup chains needs the waves.
 constexpr uint32_t kSpanBlock = MCRC_SPAN_BLOCK;
 
-template <int MODE, bool UNITS>
+// The span kernel: R = raw([ph, e)) of every work unit, pieces as they lie.
+// A unit that is a whole span stores R (span_acc[span], or out[span] without
+// a plan); a segment unit XORs M_{64Ki * (nseg-1-s)}(R) into span_acc[span].
+// k_final then turns R into the CRC or the verdict.
+template <bool UNITS>
 __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *__restrict__ img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     load_tables(smem, img, kLdsImageK1Bytes);
@@ -828,15 +838,15 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
     const uint64_t ngroups_total = (uint64_t)gridDim.x * (blockDim.x >> 5);
     uint64_t u = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
 
-    UnitDesc cur = decode_unit<MODE, UNITS>(a, fetch_unit<MODE, UNITS>(a, u, nunits, li), u, nunits, lane);
+    UnitDesc cur = decode_unit<UNITS>(a, fetch_unit<UNITS>(a, u, nunits, li), u, nunits, lane);
     // Ring of the next four units' raw records, lane-distributed: lanes
     // 8s..8s+7 of a group hold slot s.  The unit after cur is in slot sl; a
     // switch decodes it and refills the slot with the unit four further on.
     // Nothing is copied out of the ring and no load is used right after it is
     // issued (vmcnt counts in issue order: either would make the wave wait
     // for the block prefetch too).
-    uint32_t ring = fetch_unit<MODE, UNITS>(a, u + (1 + (li >> 3)) * ngroups_total, nunits, li);
-    const uint32_t *const xinv_rows = a.xinv, *const segpow_rows = a.segpow;
+    uint32_t ring = fetch_unit<UNITS>(a, u + (1 + (li >> 3)) * ngroups_total, nunits, li);
+    const uint32_t *const segpow_rows = a.segpow;
     uint32_t sl = 0;
     uint32_t k = 0;    // block index inside cur
     uint32_t acc = 0;  // lane accumulator over the blocks of cur
@@ -849,34 +859,31 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
     load_block(w0, cur, 0, li, zero);
 
     // Process the block held in `w` (block k of cur) after issuing the loads of
-    // the group's next block into `wn`.  Returns false once this group is done.
-    auto step = [&](BlockWin &w, BlockWin &wn) -> bool {
+    // the group's next block into `wn`.
+    auto step = [&](BlockWin &w, BlockWin &wn) {
         const bool last = k + 1 >= cur.niters();
-        // the unit's finishing rows (x^(i - 8t), or the segment shift), loaded
-        // before this step's other loads: the finalisation below waits for
-        // them alone, not for the block prefetch
-        // (loaded unconditionally, from a harmless row when not needed: loads
-        // under divergent branches leave the waitcnt pass a merged state that
-        // drains the prefetch)
-        const uint32_t segk = UNITS ? __shfl(cur.raw, (lane & 32u) | 7u, 64) : 0u;
-        const uint32_t *r1 = cur.single() ? xinv_rows + ((cur.eo - cur.Eo) & 15u) * 32
-                                          : segpow_rows + 32 * (segk & 255u);
-        uint32_t fx1 = 0u;
-        if (__builtin_amdgcn_readfirstlane(__any(last))) fx1 = r1[li];  // (wave-uniform branch)
-        __builtin_amdgcn_sched_barrier(0);  // (issued before the block prefetch, not sunk after it)
+        // a segment unit's shift row, loaded before this step's other loads:
+        // the multiply below waits for it alone, not for the block prefetch
+        // (under a wave-uniform branch: loads under divergent branches leave
+        // the waitcnt pass a merged state that drains the prefetch)
+        uint32_t segk = 0, fx1 = 0;
+        if (UNITS) {
+            segk = __shfl(cur.raw, (lane & 32u) | 7u, 64);
+            if (__builtin_amdgcn_readfirstlane(__any(last && !cur.single()))) fx1 = segpow_rows[32 * (segk & 255u) + li];
+            __builtin_amdgcn_sched_barrier(0);  // (issued before the block prefetch, not sunk after it)
+        }
         // next block: block k + 1 of cur, or block 0 of the unit in ring slot sl
         UnitDesc nd;
         if (__any(last)) {
             const uint32_t g = lane & 32u, sb = sl << 3;
             const uint32_t rw = __shfl(ring, g | sb | (li & 7u), 64);  // slot sl, dword li & 7
-            nd = decode_unit<MODE, UNITS>(a, rw, u + ngroups_total, nunits, lane);
+            nd = decode_unit<UNITS>(a, rw, u + ngroups_total, nunits, lane);
         }
-        if (last && (li >> 3) == sl) ring = fetch_unit<MODE, UNITS>(a, u + 5 * ngroups_total, nunits, li);
+        if (last && (li >> 3) == sl) ring = fetch_unit<UNITS>(a, u + 5 * ngroups_total, nunits, li);
         {
             UnitDesc t = cur;
             t.p = last ? nd.p : cur.p;
             t.eo = last ? nd.eo : cur.eo;
-            t.Eo = last ? nd.Eo : cur.Eo;
             t.nf = last ? nd.nf : cur.nf;
             load_block(wn, t, last ? 0u : k + 1, li, zero);
         }
@@ -891,67 +898,6 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
                 asm volatile("" ::"v"(w.v[r][q].x), "v"(w.v[r][q].y), "v"(w.v[r][q].z), "v"(w.v[r][q].w));
         if (cur.niters()) {
             const int32_t grel = (int32_t)cur.eo - (int32_t)(kBlockBytes * (cur.niters() - k));  // G - p
-            // head: zero the bytes before p and inject ~crc_in into [p, p+4).
-            // Only the lane owning the piece ph that holds p is touched (and,
-            // when p & 15 > 12, dword 0 of the next piece, which is in block 1
-            // when ph ends block 0).  The owner and the piece follow from
-            // rel = ph - q0: lane li owns it iff 0 <= rel < 4096 and
-            // rel % 1024 < 32; then it is piece (rel >> 10, (rel >> 4) & 1).
-            const uint32_t kh = (uint32_t)((uintptr_t)cur.p & 15u);
-#ifdef MCRC_ABL_NOHEAD  // ablation: skip head masking and ~crc_in injection (wrong CRCs)
-            const bool hd = false, hd2 = false;
-#else
-            const bool hd = k == 0 && cur.head();
-            const bool hd2 = cur.head() && kh > 12 && cur.Eo >= 4 && (k == 0 || (k == 1 && 16 - (int32_t)kh == grel));
-#endif
-            if (__any(hd || hd2)) {
-                const int32_t rel = -(int32_t)kh - grel - (int32_t)(kSpanCH * li), rel2 = rel + 16;  // ph - q0
-                const auto piece_of = [](int32_t x, bool en) -> int32_t {
-                    return en && x >= 0 && x < (int32_t)kBlockBytes && (x & (kRowBytes - 1)) < (int32_t)kSpanCH
-                               ? 2 * (x >> 10) + ((x >> 4) & 1)
-                               : -1;
-                };
-                const int32_t sel = piece_of(rel, hd), sel2 = piece_of(rel2, hd2);
-                const uint32_t inj = cur.Eo < 4 ? 0u : MODE == 0 ? ~__shfl(cur.raw, (lane & 32u) | 4u, 64) : 0xffffffffu;
-                const int32_t d = -(int32_t)kh;  // ph - p
-                const uint32_t m0 = keep_from(~0u, 0, kh), m1 = keep_from(~0u, 1, kh), m2 = keep_from(~0u, 2, kh),
-                               m3 = keep_from(~0u, 3, kh);
-                const uint32_t i0 = place(inj, d), i1 = place(inj, d + 4), i2 = place(inj, d + 8),
-                               i3 = place(inj, d + 12), s0 = place(inj, d + 16);
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        uint4 &v = w.v[r][j];
-                        if (sel == 2 * r + j) {
-                            v.x = (v.x & m0) ^ i0;
-                            v.y = (v.y & m1) ^ i1;
-                            v.z = (v.z & m2) ^ i2;
-                            v.w = (v.w & m3) ^ i3;
-                        }
-
-                        if (sel2 == 2 * r + j) v.x ^= s0;
-                    }
-            }
-            // tail: zero the bytes >= E in the span's last piece
-            const uint32_t te = cur.eo - cur.Eo;
-#ifdef MCRC_ABL_NOTAIL  // ablation: no tail masking (wrong CRCs)
-            const bool ht = false;
-#else
-            const bool ht = last && li == 31 && te - 1u < 15u;
-#endif
-            if (__any(ht)) {
-                // keep the first 16 - te bytes of the piece: two 64-bit masks
-                const uint32_t kt = 16u - te;
-                const uint32_t kl = kt < 8u ? kt : 8u, kq = kt > 8u ? kt - 8u : 0u;
-                const uint64_t ml = kl >= 8u ? ~0ull : (1ull << (8 * kl)) - 1ull;
-                const uint64_t mh = (1ull << (8 * kq)) - 1ull;  // kq < 8
-                uint4 &v = w.v[3][1];
-                v.x &= ht ? (uint32_t)ml : ~0u;
-                v.y &= ht ? (uint32_t)(ml >> 32) : ~0u;
-                v.z &= ht ? (uint32_t)mh : ~0u;
-                v.w &= ht ? (uint32_t)(mh >> 32) : ~0u;
-            }
             // rows wholly before p for every lane of the wave are skipped
             // (a group without a unit has niters == 0 and votes to skip)
             const uint32_t nskip = __all(grel + 3 * (int32_t)kRowBytes <= 0)   ? 3u
@@ -970,31 +916,24 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         if (last) {
             if (cur.valid()) {
 #ifdef MCRC_ABL_NOTREE  // ablation: no lane-group tree (wrong CRCs)
-                uint32_t raw = acc;
+                const uint32_t raw = acc;
 #else
-                uint32_t raw = group_reduce32_span(acc, lane);
+                const uint32_t raw = group_reduce32_span(acc, lane);
 #endif
-                if (cur.single()) {
-                    const uint32_t t = cur.eo - cur.Eo;  // tail padding
-                    const uint32_t aux = __shfl(cur.raw, (lane & 32u) | 4u, 64);
-                    const uint32_t item = UNITS ? __shfl(cur.raw, (lane & 32u) | 5u, 64) : (uint32_t)u;
-#ifndef MCRC_ABL_NOSHORT
-                    if (li == 0 && cur.Eo < 4) raw ^= short_init<MODE>(a, aux, cur.Eo, t);
-#endif
-#ifdef MCRC_ABL_NOFIN  // ablation: no x^-8t multiply (wrong CRCs)
-                    const uint32_t v = raw ^ t;
-#else
-                    const uint32_t v = mul_xinv_group(raw, fx1, li);
-#endif
-                    if (li == 0) emit<MODE>(a, item, ~v, aux, cur.sane(), cur.p);
+                if (!UNITS) {
+                    if (li == 0) a.out[u] = raw;
                 } else {
-                    // segment s of nseg: raw_v(span) gets M_{64Ki * (nseg-1-s)}(raw)
                     const uint32_t item = __shfl(cur.raw, (lane & 32u) | 5u, 64);
-                    // (the second factor, for spans past 16 MiB only, is loaded here: one
-                    // register fewer across the step, a drain only at such segment ends)
-                    uint32_t v = mul_xinv_group(raw, fx1, li);
-                    if (__any(segk >= 256u)) v = mul_xinv_group(v, segpow_rows[32 * (256 + (segk >> 8)) + li], li);
-                    if (li == 0) atomicXor(a.span_acc + item, v);
+                    if (cur.single()) {
+                        if (li == 0) a.span_acc[item] = raw;
+                    } else {
+                        // segment s of nseg: R(span) gets M_{64Ki * (nseg-1-s)}(R)
+                        // (the second factor, for spans past 16 MiB only, is loaded here:
+                        // one register fewer across the step, a drain only at such segment ends)
+                        uint32_t v = mul_row_group(raw, fx1, li);
+                        if (__any(segk >= 256u)) v = mul_row_group(v, segpow_rows[32 * (256 + (segk >> 8)) + li], li);
+                        if (li == 0) atomicXor(a.span_acc + item, v);
+                    }
                 }
             }
             acc = 0;
@@ -1005,7 +944,6 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         } else {
             ++k;
         }
-        return cur.valid();
     };
 
     // nothing issued before the loop stays pending into it (the waitcnt pass
@@ -1023,16 +961,25 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
 }
 
 // Segments per span (for the exclusive scan that places the work units), and
-// the span's item record (the header is parsed once per launch).
+// the span's item record with its z (the header is parsed once per launch, and
+// the foreign bytes of the head and tail pieces are read here: for packed
+// images they share lines with the headers this pass reads anyway).
 template <int MODE>
 __global__ void k_count(SpanArgs a, uint32_t *nseg, uint4 *irec) {
+    __shared__ uint32_t s8[256];
+    load_tab8(s8, a.tab8);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x)
     {
         const ItemDesc it = fetch_item<MODE>(a, i);
         nseg[i] = nseg_of(it.len + tail_pad(it.p, it.len));
         const uint64_t off = (uint64_t)(it.p - a.base);
-        irec[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32) | (it.sane ? 0u : kInsane), it.len, it.aux);
+        uint32_t z = 0;
+        if (it.sane) {
+            z = span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, s8, a.xpow);
+            if (MODE == 1) z ^= mulmodp_dev(~it.aux, a.xpow[tail_pad(it.p, it.len)]);  // W
+        }
+        irec[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32) | (it.sane ? 0u : kInsane), it.len, z);
         a.span_acc[i] = 0u;
     }
 }
@@ -1080,18 +1027,44 @@ __global__ void k_expand_big(const uint8_t *base, const uint32_t *nseg, const ui
     }
 }
 
-// Finalise every multi-segment span from its accumulated raw value (one
-// thread per span; the segment units already shifted and XORed their values).
-template <int MODE>
-__global__ void k_combine(SpanArgs a, const uint32_t *nseg, const uint32_t *prefix, const uint4 *irec,
-                          const uint32_t *nvalid) {
+// Every span's result from its R (one thread per span):
+//   planned (UNITS): R = span_acc[i], z from the item record: MODE 1 checks
+//   R == W, MODE 0/2 compute ~M_{-t}(R ^ Z);
+//   one unit per span (MODE 0, no plan): R = out[i], Z computed here.
+template <int MODE, bool UNITS>
+__global__ void k_final(SpanArgs a, const uint4 *irec) {
+    __shared__ uint32_t s8[256];
+    if (!UNITS) load_tab8(s8, a.tab8);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t ns = nseg[i];
-        if (ns <= 1 || prefix[i] + (uint64_t)ns > *nvalid) continue;  // single, or processed whole
-        const uint4 r = irec[i];
-        const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
-        finalize<MODE>(a, i, a.span_acc[i], r.w, a.base + off, r.z, !(r.y & kInsane));
+        const uint8_t *p;
+        uint32_t len, R, z = 0;
+        bool sane;
+        if (UNITS) {
+            const uint4 r = irec[i];
+            p = a.base + (r.x | ((uint64_t)(r.y & ~kInsane) << 32));
+            sane = !(r.y & kInsane);
+            len = r.z;
+            z = r.w;
+            R = a.span_acc[i];
+        } else {
+            const uint64_t off = a.offsets ? a.offsets[i] : i * a.stride;
+            sane = off <= a.base_bytes && a.len <= a.base_bytes - off;  // as decode_unit
+            p = a.base + (sane ? off : 0);
+            len = a.len;
+            R = a.out[i];
+            if (sane) z = span_corr(p, len, a.crc_in ? a.crc_in[i] : 0u, s8, a.xpow);
+        }
+        if (MODE == 1) {
+            const bool good = sane && R == z;
+            a.ok[i] = good;
+            if (!good) atomicAdd(a.nbad, 1ull);
+        } else {
+            const uint32_t t = tail_pad(p, len);
+            uint32_t v = R ^ z;
+            if (t) v = mulmodp_dev(v, a.xpow[kXpowInv + t]);
+            emit<MODE>(a, i, ~v, sane, p);
+        }
     }
 }
 

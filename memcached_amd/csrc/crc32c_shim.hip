@@ -67,9 +67,9 @@ struct Device {
     int cus = 0;
     bool ok = false;
     uint4 *img = nullptr;       // LDS table image of the span kernels (crc32c_gf2.h build_lds_image_span)
-    uint32_t *xinv = nullptr;   // 16 rows x^(i - 8t), i < 32: x^(-8t) spread over a lane group
+    uint32_t *tab8 = nullptr;   // byte-wise table (k_count / k_final: the foreign bytes of a span)
     uint4 *img_k1 = nullptr;    // K1 image (160 KiB, crc32c_gf2.h build_lds_image_k1)
-    uint32_t *xpow = nullptr;   // 3 x 1024 x^(8n) table
+    uint32_t *xpow = nullptr;   // x^(8n) table (layout mcrc_dev::kXpow*)
     uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
     unsigned long long *nbad = nullptr;
     hipStream_t stream = nullptr, copy = nullptr;
@@ -165,22 +165,20 @@ int init_device(Device &d, int id) {
     d.cus = p.multiProcessorCount;
     std::vector<uint32_t> img(mcrc::kImageK1Dwords);
     mcrc::build_lds_image_span(img.data(), mcrc_dev::kSpanCH);
-    std::vector<uint32_t> xinv(16 * 32);
-    for (uint32_t t = 0; t < 16; ++t) {  // x^(i - 8t): lane-distributed multiply by x^(-8t)
-        const uint32_t xi = mcrc::xpow8n_inv(t);
-        for (uint32_t i = 0; i < 32; ++i) xinv[t * 32 + i] = mcrc::mulmodp(0x80000000u >> i, xi);
-    }
-    std::vector<uint32_t> xp(3 * 1024 + 16);
+    std::vector<uint32_t> tab8(256);
+    mcrc::build_t0(tab8.data());
+    std::vector<uint32_t> xp(mcrc_dev::kXpowDwords);
     for (uint32_t j = 0; j < 1024; ++j) {
         xp[j] = mcrc::xpow8n(j);
         xp[1024 + j] = mcrc::xpow8n((uint64_t)j << 10);
         xp[2048 + j] = mcrc::xpow8n((uint64_t)j << 20);
     }
-    for (uint32_t t = 0; t < 16; ++t) xp[3072 + t] = mcrc::xpow8n_inv(t);
+    for (uint32_t t = 0; t < 16; ++t) xp[mcrc_dev::kXpowInv + t] = mcrc::xpow8n_inv(t);
+    for (uint32_t j = 0; j < 8; ++j) xp[mcrc_dev::kXpowL3 + j] = mcrc::xpow8n((uint64_t)j << 30);
     HIP_OK(hipMalloc(&d.img, img.size() * 4));
     HIP_OK(hipMemcpy(d.img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMalloc(&d.xinv, xinv.size() * 4));
-    HIP_OK(hipMemcpy(d.xinv, xinv.data(), xinv.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMalloc(&d.tab8, tab8.size() * 4));
+    HIP_OK(hipMemcpy(d.tab8, tab8.data(), tab8.size() * 4, hipMemcpyHostToDevice));
     std::vector<uint32_t> img_k1(mcrc::kImageK1Dwords);
     mcrc::build_lds_image_k1(img_k1.data(), kFixedCH);
     HIP_OK(hipMalloc(&d.img_k1, img_k1.size() * 4));
@@ -215,10 +213,8 @@ int init_device(Device &d, int id) {
     HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL(true), hipFuncAttributeMaxDynamicSharedMemorySize,
                                mcrc_dev::kLdsImageK1Bytes));
     const void *spans[] = {
-        (const void *)mcrc_dev::k_spans<0, false>,
-        (const void *)mcrc_dev::k_spans<0, true>,
-        (const void *)mcrc_dev::k_spans<1, true>,
-        (const void *)mcrc_dev::k_spans<2, true>,
+        (const void *)mcrc_dev::k_spans<false>,
+        (const void *)mcrc_dev::k_spans<true>,
     };
     for (const void *k : spans)
         HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImageK1Bytes));
@@ -294,16 +290,18 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     (void)aligned;
     auto spans = [&](const mcrc_dev::SpanArgs &x, int grid) {
         if (x.units)
-            hipLaunchKernelGGL((mcrc_dev::k_spans<MODE, true>), dim3(grid), dim3(mcrc_dev::kSpanBlock),
+            hipLaunchKernelGGL((mcrc_dev::k_spans<true>), dim3(grid), dim3(mcrc_dev::kSpanBlock),
                                mcrc_dev::kLdsImageK1Bytes, st, x, d.img);
         else
-            hipLaunchKernelGGL((mcrc_dev::k_spans<MODE, false>), dim3(grid), dim3(mcrc_dev::kSpanBlock),
+            hipLaunchKernelGGL((mcrc_dev::k_spans<false>), dim3(grid), dim3(mcrc_dev::kSpanBlock),
                                mcrc_dev::kLdsImageK1Bytes, st, x, d.img);
     };
+    const int g1 = (int)std::min<uint64_t>((n + 255) / 256, 4096);
     if (identity) {
         spans(a, grid_for(d, n));
+        hipLaunchKernelGGL((mcrc_dev::k_final<0, false>), dim3(g1), dim3(256), 0, st, a, nullptr);
         HIP_OK(hipGetLastError());
-    return CRC32C_OK;
+        return CRC32C_OK;
     }
     if (n >= 0xffffffffull) return CRC32C_EINVAL;
     // units fit in cap whenever the spans do not overlap; overlapping long spans
@@ -312,7 +310,6 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     int rc = ensure_plan(d, n, cap);
     if (rc) return rc;
     uint32_t *nvalid = d.counters, *nwhole = d.counters + 1, *nbig = d.counters + 2;
-    const int g1 = (int)std::min<uint64_t>((n + 255) / 256, 4096);
     HIP_OK(hipMemsetAsync(nvalid, 0xff, 4, st));
     HIP_OK(hipMemsetAsync(nwhole, 0, 8, st));  // nwhole, nbig
     a.span_acc = d.span_acc;
@@ -333,7 +330,7 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     w.units = d.whole;
     w.nunits = nwhole;
     spans(w, d.cus);
-    hipLaunchKernelGGL((mcrc_dev::k_combine<MODE>), dim3(g1), dim3(256), 0, st, u, d.nseg, d.prefix, d.irec, nvalid);
+    hipLaunchKernelGGL((mcrc_dev::k_final<MODE, true>), dim3(g1), dim3(256), 0, st, u, d.irec);
     HIP_OK(hipGetLastError());
     return CRC32C_OK;
 }
@@ -374,15 +371,13 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
     a.stride = s.stride;
     a.lens = s.lens;
     a.len = s.len;
-    if (s.lens == nullptr)
-        for (uint32_t t = 0; t < 16; ++t) a.kspan16[t] = mcrc::xpow8n((uint64_t)s.len + t);
     a.crc_in = s.crc_in;
     a.out = s.out;
     a.nbad = d.nbad;  // spans outside the buffer
     a.n = s.n;
     a.segpow = d.segpow;
     a.xpow = d.xpow;
-    a.xinv = d.xinv;
+    a.tab8 = d.tab8;
     a.zero = d.zero;
     HIP_OK(hipMemsetAsync(d.nbad, 0, sizeof(unsigned long long), st));
     const bool aligned = (flags & CRC32C_ALIGNED16) ||
@@ -615,7 +610,7 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
     a.nbad = d->nbad;
     a.n = n;
     a.xpow = d->xpow;
-    a.xinv = d->xinv;
+    a.tab8 = d->tab8;
     a.zero = d->zero;
     a.region = region_bytes;
     d->acquire(st);
@@ -871,7 +866,7 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     a.nbad = d->nbad;
     a.n = total;
     a.xpow = d->xpow;
-    a.xinv = d->xinv;
+    a.tab8 = d->tab8;
     a.zero = d->zero;
     a.region = wbuf_bytes;
     HIP_OK(hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st));
