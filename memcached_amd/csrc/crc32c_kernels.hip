@@ -497,7 +497,7 @@ struct SpanArgs {
     uint64_t n;                // spans (items)
     const uint32_t *xpow;      // x^(8*j), x^(8*1024*j), x^(8*2^20*j) (3 x 1024), x^(-8t) (16),
                                // x^(8*2^30*j) (8): layout kXpow*
-    const uint32_t *tab8;      // byte-wise table (crc32c_table_little[0], crc32c.c:399), 256 entries
+    const uint32_t *tab8;      // 4 x 256 byte tables (Tab8)
     const uint4 *zero;         // kZeroBytes of zeros in device memory
     // work units (nullptr: unit u = span u, one segment)
     const struct UnitRec *units;
@@ -558,33 +558,115 @@ __device__ __forceinline__ Piece shl_bytes(Piece v, uint32_t s) {
     if (s == 0) return v;
     return {v.lo << (8 * s), (v.hi << (8 * s)) | (v.lo >> (64 - 8 * s))};
 }
-// Register after the 16 bytes of v from a zero register (the byte-wise loop
-// of crc32c.c:399, t8 = its table crc32c_table_little[0]).
-__device__ __forceinline__ uint32_t raw16(Piece v, const uint32_t *t8) {
+// Byte tables in LDS for the per-thread work of k_count / k_final: [0] is
+// crc32c.c:399's byte-wise table (crc32c_table_little[0]), [k] the same
+// followed by k zero bytes, so a dword is one slice-by-4 step (crc32c.c:401-415's
+// form).  (A copy per bank, conflict-free but four dependent lookups per dword,
+// measured slower: the per-thread chains are latency-bound.)
+struct Tab8 {
+    const uint32_t *s;
+    __device__ __forceinline__ uint32_t step(uint32_t r) const { return s[r & 255u] ^ (r >> 8); }
+    __device__ __forceinline__ uint32_t dword(uint32_t r, uint32_t d) const {
+        r ^= d;
+        return s[768 + (r & 255u)] ^ s[512 + ((r >> 8) & 255u)] ^ s[256 + ((r >> 16) & 255u)] ^ s[r >> 24];
+    }
+};
+constexpr uint32_t kTab8Dwords = 4 * 256;
+// (every thread of the block calls it)
+__device__ __forceinline__ Tab8 load_tab8(uint32_t *s, const uint32_t *tab8) {
+    for (uint32_t i = threadIdx.x; i < kTab8Dwords; i += blockDim.x) s[i] = tab8[i];
+    __syncthreads();
+    return {s};
+}
+
+// Register after the 16 bytes of v from a zero register.
+__device__ __forceinline__ uint32_t raw16(Piece v, const Tab8 &t) {
     uint32_t r = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        r ^= (uint32_t)((k < 2 ? v.lo : v.hi) >> (32 * (k & 1)));
-#pragma unroll
-        for (int b = 0; b < 4; ++b) r = t8[r & 255u] ^ (r >> 8);
+    for (int k = 0; k < 4; ++k) r = t.dword(r, (uint32_t)((k < 2 ? v.lo : v.hi) >> (32 * (k & 1))));
+    return r;
+}
+
+// Byte b (dynamic, < 16) of a piece.
+__device__ __forceinline__ uint32_t byte_of(Piece v, uint32_t b) {
+    return (uint32_t)(b < 8 ? v.lo >> (8 * b) : v.hi >> (8 * (b - 8))) & 255u;
+}
+// Register r advanced over the n bytes at p (one thread): the partial first
+// and last 16-B pieces byte by byte, whole pieces dword by dword.  Every
+// load is an aligned piece holding a byte of [p, p + n).
+__device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, uint32_t n, const Tab8 &t) {
+    if (n == 0) return r;
+    const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
+    const uint8_t *q = p - kh;
+    Piece v = ld_piece(q);
+    const uint32_t b1 = kh + n < 16u ? kh + n : 16u;
+    for (uint32_t b = kh; b < b1; ++b) r = t.step(r ^ byte_of(v, b));
+    n -= b1 - kh;
+    q += 16;
+#pragma unroll 8
+    for (; n >= 16; n -= 16, q += 16) {
+        v = ld_piece(q);
+        r = t.dword(r, (uint32_t)v.lo);
+        r = t.dword(r, (uint32_t)(v.lo >> 32));
+        r = t.dword(r, (uint32_t)v.hi);
+        r = t.dword(r, (uint32_t)(v.hi >> 32));
+    }
+    if (n) {
+        v = ld_piece(q);
+        for (uint32_t b = 0; b < n; ++b) r = t.step(r ^ byte_of(v, b));
     }
     return r;
 }
 
-// Z of span [p, p + len) with initial CRC c (see "Pieces as they lie"):
-//   crc32c(c, D) = ~M_{-t}(R ^ Z),  Z = M_{len+t}(~c ^ raw(F_h)) ^ raw(F_t).
-// raw(F_h) = raw of the head piece's first kh bytes moved to its top (leading
-// zeros leave a zero register unchanged); raw(F_t) = raw of the tail piece
-// with its first 16 - t bytes cleared.  A span without bytes is not read by
-// the span kernel (R = 0): Z = M_t(~c).  One thread; t8 in LDS.
-__device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, uint32_t c, const uint32_t *t8,
+// Head fragment.  The block grid of a span is anchored at Ea, 4 KiB apart
+// (segments are whole numbers of blocks, so every unit of the span uses the
+// same grid); G1 = the first grid point after ph.  The span kernel would
+// spend a whole block step of its group on [p, G1), mostly on rows without a
+// byte of the span; when G1 - p <= kFragMax the span's thread takes those
+// bytes instead (reg_advance), the head unit starts at G1, and a span that
+// fits one block is not given to the span kernel at all.
+#ifndef MCRC_FRAG_MAX
+#define MCRC_FRAG_MAX 1024
+#endif
+constexpr uint32_t kFragMax = MCRC_FRAG_MAX;
+struct SpanHead {
+    uint64_t g1o;  // G1 - p
+    bool drop;     // [p, G1) is the thread's
+};
+__device__ __forceinline__ SpanHead span_head(const uint8_t *p, uint32_t len) {
+    const uint64_t kh = (uintptr_t)p & 15u;
+    const uint64_t x = (uint64_t)len + tail_pad(p, len) + kh;  // Ea - ph
+    const uint64_t g1o = x - kBlockBytes * ((x - 1) / kBlockBytes) - kh;
+    return {g1o, len != 0 && g1o <= kFragMax};
+}
+
+// Z of span [p, p + len) with initial CRC c (see "Pieces as they lie"), for
+// the R that the span kernel computes over the span's units:
+// - no bytes: the kernel reads nothing (R = 0), Z = M_t(~c);
+// - head fragment taken (span_head): the kernel reads [G1, Ea), so
+//   Z = M_{Ea-G1}(r) ^ raw(F_t) with r = the register from ~c over [p, G1),
+//   or, when G1 = Ea, Z = M_t(register from ~c over D);
+// - otherwise Z = M_{len+t}(~c ^ raw(F_h)) ^ raw(F_t): raw(F_h) = raw of the
+//   head piece's first kh bytes moved to its top (leading zeros leave a zero
+//   register unchanged), raw(F_t) = raw of the tail piece with its first
+//   16 - t bytes cleared.
+// One thread.
+__device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
                                               const uint32_t *xp) {
     const uint32_t t = tail_pad(p, len);
     if (len == 0) return mulmodp_dev(~c, xp[t]);
-    const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
-    uint32_t y = ~c;
-    if (kh) y ^= raw16(shl_bytes(ld_piece(p - kh), 16 - kh), t8);
-    uint32_t z = mulmodp_dev(y, xpow8_dev(xp, (uint64_t)len + t));
+    const uint64_t vlen = (uint64_t)len + t;
+    const SpanHead h = span_head(p, len);
+    if (h.drop && h.g1o == vlen) return mulmodp_dev(reg_advance(~c, p, len, t8), xp[t]);
+    uint32_t z;
+    if (h.drop) {
+        z = mulmodp_dev(reg_advance(~c, p, (uint32_t)h.g1o, t8), xpow8_dev(xp, vlen - h.g1o));
+    } else {
+        const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
+        uint32_t y = ~c;
+        if (kh) y ^= raw16(shl_bytes(ld_piece(p - kh), 16 - kh), t8);
+        z = mulmodp_dev(y, xpow8_dev(xp, vlen));
+    }
     if (t) {
         const Piece v = ld_piece(p + len + t - 16);
         const Piece m = shl_bytes({~0ull, ~0ull}, 16 - t);
@@ -593,11 +675,7 @@ __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, ui
     return z;
 }
 
-// The byte table into LDS (k_count, k_final: 256-thread blocks).
-__device__ __forceinline__ void load_tab8(uint32_t *s8, const uint32_t *tab8) {
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) s8[i] = tab8[i];
-    __syncthreads();
-}
+
 
 template <int MODE>
 __device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
@@ -611,14 +689,26 @@ __device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
         d.len = d.sane ? len : 0u;
         d.aux = a.crc_in ? a.crc_in[i] : 0u;
     } else {
-        // item header fields (memcached.h:613-636), ITEM_ntotal (:149-152)
+        // item header fields (memcached.h:613-636), ITEM_ntotal (:149-152):
+        // bytes 28..41 of the image from the two aligned pieces holding them
         const uint8_t *it = a.base + off;
         const bool hdr_ok = off + 48 <= a.base_bytes;
-        const uint32_t nbytes = hdr_ok ? ld_u32_unaligned(it + 32) : 0u;
-        const uint32_t flags = hdr_ok ? (ld_u8(it + 38) | (ld_u8(it + 39) << 8)) : 0u;
-        const uint32_t nkey = hdr_ok ? ld_u8(it + 41) : 0u;
+        uint64_t f0 = 0, f1 = 0;  // image bytes 28..35, 36..43
+        if (hdr_ok) {
+            const uintptr_t x = (uintptr_t)(it + 28), q = x & ~(uintptr_t)15, q2 = (x + 13) & ~(uintptr_t)15;
+            const Piece v0 = ld_piece((const uint8_t *)q), v1 = ld_piece((const uint8_t *)q2);
+            const uint32_t sh = (uint32_t)(x - q);  // 0..15
+            const uint64_t w0 = v0.lo, w1 = v0.hi, w2 = q2 != q ? v1.lo : 0, w3 = q2 != q ? v1.hi : 0;
+            const uint64_t a0 = sh < 8 ? w0 : w1, a1 = sh < 8 ? w1 : w2, a2 = sh < 8 ? w2 : w3;
+            const uint32_t k = 8 * (sh & 7u);
+            f0 = k ? (a0 >> k) | (a1 << (64 - k)) : a0;
+            f1 = k ? (a1 >> k) | (a2 << (64 - k)) : a1;
+        }
+        const uint32_t nbytes = (uint32_t)(f0 >> 32);
+        const uint32_t flags = (uint32_t)(f1 >> 16) & 0xffffu;
+        const uint32_t nkey = (uint32_t)(f1 >> 40) & 0xffu;
         const uint64_t ntotal = 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) + ((flags & 2u) ? 8 : 0);
-        d.aux = hdr_ok ? ld_u32_unaligned(it + 28) : 0u;
+        d.aux = (uint32_t)f0;
         // an item never crosses its write buffer (extstore.c:627-636), so a
         // header claiming otherwise is corrupt
         const bool in_region = a.region == 0 || off / a.region == (off + ntotal - 1) / a.region;
@@ -664,7 +754,11 @@ __device__ __forceinline__ UnitRec make_unit(const uint8_t *base, uint64_t off, 
     const uint32_t nseg = seg == kWhole ? 1u : nseg_of(vlen);
     const bool single = nseg == 1, head = single || seg == 0;
     const uint32_t eo0 = vlen - (single ? 0u : (nseg - 1 - seg) * kSegBytes);  // e - p0
-    const uint32_t po = head ? 0u : eo0 - kSegBytes;                          // p - p0
+    uint32_t po = head ? 0u : eo0 - kSegBytes;                                // p - p0
+    if (head) {  // a head fragment taken by the span's thread: the unit starts at G1
+        const SpanHead h = span_head(p0, len);
+        if (h.drop) po = (uint32_t)h.g1o;
+    }
     const uint32_t eo = eo0 - po;
     const uint32_t niters = len ? (eo + (uint32_t)((uintptr_t)(p0 + po) & 15u) + kBlockBytes - 1) / kBlockBytes : 0u;
     const uint64_t o = off + po;
@@ -776,17 +870,15 @@ __device__ __forceinline__ uint32_t block_value(const BlockWin &w, const LaneCtx
 // Stamp writes the spill CRC into the image's exptime field, bytes 28..31 =
 // p - 4 (storage.c:567), or into out[] when the caller stages the images (host
 // path); ok[] (if any) marks stamped images.  A span that is not sane (outside
-// the buffer, or a malformed image) was not read: counted in nbad.
+// the buffer, or a malformed image) was not read (the caller counts it).
 template <int MODE>
 __device__ __forceinline__ void emit(const SpanArgs &a, uint64_t item, uint32_t crc, bool sane, const uint8_t *p) {
     if (MODE == 0) {
         a.out[item] = sane ? crc : 0u;
-        if (!sane) atomicAdd(a.nbad, 1ull);
     } else {
         if (a.ok) a.ok[item] = sane;
-        if (!sane) {
-            atomicAdd(a.nbad, 1ull);
-        } else if (a.out) {
+        if (!sane) return;
+        if (a.out) {
             a.out[item] = crc;
         } else {
             uint8_t *x = const_cast<uint8_t *>(p) - 4;
@@ -960,23 +1052,33 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
     }
 }
 
-// Segments per span (for the exclusive scan that places the work units), and
+// Work units of span [p, p + len): its segments, less a head segment that
+// was one block and whose fragment the span's thread takes (none for len 0).
+__device__ __forceinline__ uint32_t span_units(const uint8_t *p, uint32_t len) {
+    if (len == 0) return 0;
+    const uint32_t vlen = len + tail_pad(p, len);
+    const uint32_t ns = nseg_of(vlen);
+    const SpanHead h = span_head(p, len);
+    return ns - (h.drop && h.g1o == vlen - (uint64_t)(ns - 1) * kSegBytes ? 1u : 0u);
+}
+
+// Units per span (for the exclusive scan that places the work units), and
 // the span's item record with its z (the header is parsed once per launch, and
 // the foreign bytes of the head and tail pieces are read here: for packed
 // images they share lines with the headers this pass reads anyway).
 template <int MODE>
-__global__ void k_count(SpanArgs a, uint32_t *nseg, uint4 *irec) {
-    __shared__ uint32_t s8[256];
-    load_tab8(s8, a.tab8);
+__global__ void k_count(SpanArgs a, uint32_t *nunit, uint4 *irec) {
+    __shared__ uint32_t s8[kTab8Dwords];
+    const Tab8 t8 = load_tab8(s8, a.tab8);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x)
     {
         const ItemDesc it = fetch_item<MODE>(a, i);
-        nseg[i] = nseg_of(it.len + tail_pad(it.p, it.len));
+        nunit[i] = span_units(it.p, it.len);
         const uint64_t off = (uint64_t)(it.p - a.base);
         uint32_t z = 0;
         if (it.sane) {
-            z = span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, s8, a.xpow);
+            z = span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow);
             if (MODE == 1) z ^= mulmodp_dev(~it.aux, a.xpow[tail_pad(it.p, it.len)]);  // W
         }
         irec[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32) | (it.sane ? 0u : kInsane), it.len, z);
@@ -991,40 +1093,68 @@ __global__ void k_count(SpanArgs a, uint32_t *nseg, uint4 *irec) {
 // and expanded by k_expand_big, one workgroup per span.
 constexpr uint32_t kExpandInline = 32;
 
-__global__ void k_expand(const uint8_t *base, const uint32_t *nseg, const uint32_t *prefix, const uint4 *irec,
+// First segment of span i that is a unit (1 when the head segment is not).
+__device__ __forceinline__ uint32_t first_seg(const uint8_t *p, uint32_t len, uint32_t nunit) {
+    return nunit ? nseg_of(len + tail_pad(p, len)) - nunit : 0u;
+}
+
+__global__ void k_expand(const uint8_t *base, const uint32_t *nunit, const uint32_t *prefix, const uint4 *irec,
                          uint64_t n, UnitRec *units, uint64_t cap, uint32_t *nvalid, UnitRec *whole,
                          uint32_t *nwhole, uint32_t *big, uint32_t *nbig) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t p0 = prefix[i], ns = nseg[i];
+        const uint64_t p0 = prefix[i], ns = nunit[i];
         const uint4 r = irec[i];
         const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
         const bool sane = !(r.y & kInsane);
         if (p0 + ns <= cap) {
+            const uint32_t s0 = first_seg(base + off, r.z, (uint32_t)ns);
             if (ns > kExpandInline)
                 big[atomicAdd(nbig, 1u)] = (uint32_t)i;
             else
-                for (uint32_t s = 0; s < ns; ++s) units[p0 + s] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, s);
+                for (uint32_t s = 0; s < ns; ++s)
+                    units[p0 + s] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, s0 + s);
             if (i + 1 == n) *nvalid = (uint32_t)(p0 + ns);
         } else {
             if (p0 <= cap) atomicMin(nvalid, (uint32_t)p0);
+            // (one unit with the span's head rule: the same grid, so the same G1)
             whole[atomicAdd(nwhole, 1u)] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, kWhole);
         }
     }
 }
 
-__global__ void k_expand_big(const uint8_t *base, const uint32_t *nseg, const uint32_t *prefix, const uint4 *irec,
+__global__ void k_expand_big(const uint8_t *base, const uint32_t *nunit, const uint32_t *prefix, const uint4 *irec,
                              UnitRec *units, const uint32_t *big, const uint32_t *nbig) {
     const uint32_t nb = *nbig;
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint32_t i = big[b];
         const uint64_t p0 = prefix[i];
-        const uint32_t ns = nseg[i];
+        const uint32_t ns = nunit[i];
         const uint4 r = irec[i];
         const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
+        const uint32_t s0 = first_seg(base + off, r.z, ns);
         for (uint32_t s = threadIdx.x; s < ns; s += blockDim.x)
-            units[p0 + s] = make_unit(base, off, r.z, r.w, !(r.y & kInsane), i, s);
+            units[p0 + s] = make_unit(base, off, r.z, r.w, !(r.y & kInsane), i, s0 + s);
     }
+}
+
+// nbad += the per-thread counts of a workgroup: one atomic per workgroup.
+// (Atomics on one address serialise in L2: one per bad item of a verify with
+// 1 % corrupt items took 0.4 ms per 300 pages.)  Every thread of the block
+// calls it.
+__device__ __forceinline__ void count_bad(unsigned long long *nbad, uint32_t nb) {
+    __shared__ uint32_t sum;
+    if (threadIdx.x == 0) sum = 0;
+    __syncthreads();
+    nb += __shfl_xor(nb, 1);
+    nb += __shfl_xor(nb, 2);
+    nb += __shfl_xor(nb, 4);
+    nb += __shfl_xor(nb, 8);
+    nb += __shfl_xor(nb, 16);
+    nb += __shfl_xor(nb, 32);
+    if (__lane_id() == 0 && nb) atomicAdd(&sum, nb);
+    __syncthreads();
+    if (threadIdx.x == 0 && sum) atomicAdd(nbad, (unsigned long long)sum);
 }
 
 // Every span's result from its R (one thread per span):
@@ -1033,8 +1163,10 @@ __global__ void k_expand_big(const uint8_t *base, const uint32_t *nseg, const ui
 //   one unit per span (MODE 0, no plan): R = out[i], Z computed here.
 template <int MODE, bool UNITS>
 __global__ void k_final(SpanArgs a, const uint4 *irec) {
-    __shared__ uint32_t s8[256];
-    if (!UNITS) load_tab8(s8, a.tab8);
+    __shared__ uint32_t s8[UNITS ? 1 : kTab8Dwords];
+    Tab8 t8{s8};
+    if (!UNITS) t8 = load_tab8(s8, a.tab8);
+    uint32_t nb = 0;  // bad spans seen by this thread
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint8_t *p;
@@ -1052,20 +1184,23 @@ __global__ void k_final(SpanArgs a, const uint4 *irec) {
             sane = off <= a.base_bytes && a.len <= a.base_bytes - off;  // as decode_unit
             p = a.base + (sane ? off : 0);
             len = a.len;
-            R = a.out[i];
-            if (sane) z = span_corr(p, len, a.crc_in ? a.crc_in[i] : 0u, s8, a.xpow);
+            const SpanHead h = span_head(p, len);
+            R = sane && !(h.drop && h.g1o == len + tail_pad(p, len)) ? a.out[i] : 0u;  // (else not given to k_spans)
+            if (sane) z = span_corr(p, len, a.crc_in ? a.crc_in[i] : 0u, t8, a.xpow);
         }
         if (MODE == 1) {
             const bool good = sane && R == z;
             a.ok[i] = good;
-            if (!good) atomicAdd(a.nbad, 1ull);
+            nb += !good;
         } else {
             const uint32_t t = tail_pad(p, len);
             uint32_t v = R ^ z;
             if (t) v = mulmodp_dev(v, a.xpow[kXpowInv + t]);
             emit<MODE>(a, i, ~v, sane, p);
+            nb += !sane;
         }
     }
+    count_bad(a.nbad, nb);
 }
 
 // Chained CRC over an iov list (the chunked-item read verify of

@@ -67,7 +67,7 @@ struct Device {
     int cus = 0;
     bool ok = false;
     uint4 *img = nullptr;       // LDS table image of the span kernels (crc32c_gf2.h build_lds_image_span)
-    uint32_t *tab8 = nullptr;   // byte-wise table (k_count / k_final: the foreign bytes of a span)
+    uint32_t *tab8 = nullptr;   // byte-wise table (k_count / k_final: a span's head fragment and foreign bytes)
     uint4 *img_k1 = nullptr;    // K1 image (160 KiB, crc32c_gf2.h build_lds_image_k1)
     uint32_t *xpow = nullptr;   // x^(8n) table (layout mcrc_dev::kXpow*)
     uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
@@ -100,7 +100,7 @@ struct Device {
     uint32_t *hlens[2] = {nullptr, nullptr}, *hcin[2] = {nullptr, nullptr}, *hout[2] = {nullptr, nullptr};
     uint64_t slot_items = 0;
     // work-unit planning for long / variable spans (grow-only)
-    uint32_t *nseg = nullptr, *prefix = nullptr, *span_acc = nullptr, *counters = nullptr;
+    uint32_t *nunit = nullptr, *prefix = nullptr, *span_acc = nullptr, *counters = nullptr;
     uint32_t *segpow = nullptr;  // rows x^i * x^(8*64Ki*k): k < 256, then k = 256 j
     mcrc_dev::UnitRec *units = nullptr, *whole = nullptr;
     uint4 *irec = nullptr;  // per-span record written by k_count
@@ -165,8 +165,12 @@ int init_device(Device &d, int id) {
     d.cus = p.multiProcessorCount;
     std::vector<uint32_t> img(mcrc::kImageK1Dwords);
     mcrc::build_lds_image_span(img.data(), mcrc_dev::kSpanCH);
-    std::vector<uint32_t> tab8(256);
+    std::vector<uint32_t> tab8(1024);  // [k][b]: the byte-wise table followed by k zero bytes
     mcrc::build_t0(tab8.data());
+    for (uint32_t k = 1; k < 4; ++k) {
+        const mcrc::Gf2Op zk = mcrc::Gf2Op::zeros(k);
+        for (uint32_t b = 0; b < 256; ++b) tab8[256 * k + b] = zk.apply(tab8[b]);
+    }
     std::vector<uint32_t> xp(mcrc_dev::kXpowDwords);
     for (uint32_t j = 0; j < 1024; ++j) {
         xp[j] = mcrc::xpow8n(j);
@@ -250,20 +254,20 @@ bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
 int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
     if (d.plan_items < n) {
-        (void)hipFree(d.nseg);
+        (void)hipFree(d.nunit);
         (void)hipFree(d.prefix);
         (void)hipFree(d.whole);
         (void)hipFree(d.irec);
         (void)hipFree(d.span_acc);
         (void)hipFree(d.big);
         d.plan_items = 0;
-        if (hipMalloc(&d.nseg, n * 4) != hipSuccess || hipMalloc(&d.prefix, n * 4) != hipSuccess ||
+        if (hipMalloc(&d.nunit, n * 4) != hipSuccess || hipMalloc(&d.prefix, n * 4) != hipSuccess ||
             hipMalloc(&d.whole, n * sizeof(mcrc_dev::UnitRec)) != hipSuccess ||
             hipMalloc(&d.irec, n * sizeof(uint4)) != hipSuccess || hipMalloc(&d.span_acc, n * 4) != hipSuccess ||
             hipMalloc(&d.big, n * 4) != hipSuccess)
             return CRC32C_ENOMEM;
         size_t need = 0;
-        if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, d.nseg, d.prefix, (int)n) != hipSuccess)
+        if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, d.nunit, d.prefix, (int)n) != hipSuccess)
             return CRC32C_EHIP;
         if (need > d.scan_tmp_bytes) {
             (void)hipFree(d.scan_tmp);
@@ -298,7 +302,8 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     };
     const int g1 = (int)std::min<uint64_t>((n + 255) / 256, 4096);
     if (identity) {
-        spans(a, grid_for(d, n));
+        // (spans of at most kFragMax - 15 bytes are all their threads' in k_final)
+        if (a.len + 15 > mcrc_dev::kFragMax) spans(a, grid_for(d, n));
         hipLaunchKernelGGL((mcrc_dev::k_final<0, false>), dim3(g1), dim3(256), 0, st, a, nullptr);
         HIP_OK(hipGetLastError());
         return CRC32C_OK;
@@ -313,12 +318,12 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     HIP_OK(hipMemsetAsync(nvalid, 0xff, 4, st));
     HIP_OK(hipMemsetAsync(nwhole, 0, 8, st));  // nwhole, nbig
     a.span_acc = d.span_acc;
-    hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nseg, d.irec);
+    hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nunit, d.irec);
     size_t tmp = d.scan_tmp_bytes;
-    HIP_OK(hipcub::DeviceScan::ExclusiveSum(d.scan_tmp, tmp, d.nseg, d.prefix, (int)n, st));
-    hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(g1), dim3(256), 0, st, a.base, d.nseg, d.prefix, d.irec, n, d.units,
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(d.scan_tmp, tmp, d.nunit, d.prefix, (int)n, st));
+    hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(g1), dim3(256), 0, st, a.base, d.nunit, d.prefix, d.irec, n, d.units,
                        cap, nvalid, d.whole, nwhole, d.big, nbig);
-    hipLaunchKernelGGL(mcrc_dev::k_expand_big, dim3(1024), dim3(256), 0, st, a.base, d.nseg, d.prefix, d.irec,
+    hipLaunchKernelGGL(mcrc_dev::k_expand_big, dim3(1024), dim3(256), 0, st, a.base, d.nunit, d.prefix, d.irec,
                        d.units, d.big, nbig);
     mcrc_dev::SpanArgs u = a;
     u.units = d.units;
