@@ -1,0 +1,130 @@
+"""Integer restatement of the span kernels' work-unit geometry and of the
+per-span correction (memcached_amd/csrc/crc32c_kernels.hip: nseg_of,
+span_head, span_units, make_unit, load_block, span_corr).  Test
+infrastructure: the CPU tests check the addressing and the algebra with it,
+without a GPU."""
+SEG = 64 * 1024
+BLOCK = 4096
+WHOLE = 0xFFFFFFFF
+FRAG_MAX = 1024
+POLY = 0x82F63B78
+M32 = 0xFFFFFFFF
+
+
+def tail_pad(p, length):
+    return (-(p + length)) & 15
+
+
+def nseg_of(vlen):
+    return 1 if vlen <= SEG + 16 else (vlen - 16 + SEG - 1) // SEG
+
+
+def span_head(p, length):
+    """(G1 - p, drop): G1 = the first point of the span's 4 KiB grid (anchored
+    at Ea) after ph; drop = the head fragment [p, G1) is the span thread's."""
+    kh = p & 15
+    x = length + tail_pad(p, length) + kh
+    g1o = x - BLOCK * ((x - 1) // BLOCK) - kh if length else 0
+    return g1o, length != 0 and g1o <= FRAG_MAX
+
+
+def span_units(p, length):
+    if length == 0:
+        return 0
+    vlen = length + tail_pad(p, length)
+    ns = nseg_of(vlen)
+    g1o, drop = span_head(p, length)
+    return ns - (1 if drop and g1o == vlen - (ns - 1) * SEG else 0)
+
+
+def first_seg(p, length, nunit):
+    return nseg_of(length + tail_pad(p, length)) - nunit if nunit else 0
+
+
+def make_unit(base, off, length, seg):
+    """(p, eo = e - p, niters, single, segk) of one work unit."""
+    p0 = base + off
+    vlen = length + tail_pad(p0, length)
+    nseg = 1 if seg == WHOLE else nseg_of(vlen)
+    single = nseg == 1
+    head = single or seg == 0
+    eo0 = vlen - (0 if single else (nseg - 1 - seg) * SEG)
+    po = 0 if head else eo0 - SEG
+    if head:
+        g1o, drop = span_head(p0, length)
+        if drop:
+            po = g1o
+    eo = eo0 - po
+    niters = (eo + ((p0 + po) & 15) + BLOCK - 1) // BLOCK if length else 0
+    return p0 + po, eo, niters, single, 0 if single else nseg - 1 - seg
+
+
+def units_of(base, off, length):
+    """The work units k_expand writes for a span."""
+    nu = span_units(base + off, length)
+    s0 = first_seg(base + off, length, nu)
+    return [make_unit(base, off, length, s0 + s) for s in range(nu)]
+
+
+def real_pieces(p, eo, niters, k):
+    """Addresses of the pieces load_block reads from memory for block k."""
+    grel = eo - BLOCK * (niters - k)
+    out = []
+    for li in range(32):
+        lrel = grel + 32 * li
+        e0 = lrel + 16 + (p & 15) if niters else -BLOCK - 16
+        for r in range(4):
+            er = e0 + 1024 * r
+            if er > 0:
+                out.append(p + lrel + 1024 * r)
+            if er + 16 > 0:
+                out.append(p + lrel + 1024 * r + 16)
+    return out
+
+
+# --- GF(2) arithmetic (crc32c.c:58-137's algebra, reflected basis) ---------
+
+def mulmodp(a, b):
+    prod = 0
+    for i in range(31, -1, -1):
+        if (a >> i) & 1:
+            prod ^= b
+        b = (b >> 1) ^ (POLY if b & 1 else 0)
+    return prod
+
+
+def xpow8(n):
+    r, sq = 0x80000000, 0x00800000
+    while n:
+        if n & 1:
+            r = mulmodp(r, sq)
+        n >>= 1
+        if n:
+            sq = mulmodp(sq, sq)
+    return r
+
+
+_INV = {}
+
+
+def xpow8_inv(t):
+    """x^(-8t): the y with y * x^(8t) = 1 (solved over GF(2))."""
+    if t not in _INV:
+        a = xpow8(t)
+        basis = {}
+        for i in range(32):
+            v, comb = mulmodp(1 << i, a), 1 << i
+            for bit in sorted(basis, reverse=True):
+                if (v >> bit) & 1:
+                    v ^= basis[bit][0]
+                    comb ^= basis[bit][1]
+            if v:
+                basis[v.bit_length() - 1] = (v, comb)
+        target, comb = 0x80000000, 0
+        for bit in sorted(basis, reverse=True):
+            if (target >> bit) & 1:
+                target ^= basis[bit][0]
+                comb ^= basis[bit][1]
+        assert target == 0
+        _INV[t] = comb
+    return _INV[t]

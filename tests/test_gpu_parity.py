@@ -488,6 +488,25 @@ def test_offsets_with_fixed_length(torch):
     np.testing.assert_array_equal(outh, oracle.batch(host, offs, np.full(n, L)))
 
 
+@pytest.mark.parametrize("L", [1, 15, 100, 1008, 1009, 1010, 1024, 1040, 4080, 4097, 5104, 5125, 8195, 65536, 65552])
+def test_fixed_length_head_fragment_thresholds(torch, L):
+    """offsets[] with one shared length (one unit per span, no plan) at the
+    lengths where the head fragment moves between the span kernel and the
+    span's thread (kFragMax = 1024) or the span skips the kernel entirely."""
+    import ctypes
+    rng = np.random.default_rng(L)
+    n = 700
+    size = n * (L + 40) + 64
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    offs = np.sort(rng.integers(0, size - L, n)).astype(np.uint64)
+    cin = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    d, doffs, dcin = _dev(torch, host), _dev(torch, offs.view(np.int64)), _dev(torch, cin.view(np.int32))
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = _lib.Spans(d.data_ptr(), host.size, doffs.data_ptr(), 0, None, L, dcin.data_ptr(), out.data_ptr(), n)
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(s), _lib.CRC32C_DEVICE, None))
+    np.testing.assert_array_equal(_u32(out), oracle.batch(host, offs, np.full(n, L), cin))
+
+
 @pytest.mark.parametrize("name", ["cfg1", "varied"])
 def test_verify_golden_items(torch, name):
     g = np.load(os.path.join(GOLD, "items.npz"))
