@@ -799,14 +799,24 @@ __device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw,
         d.eo = __shfl(raw, g | 2, 64);
         d.nf = __shfl(raw, g | 6, 64);
     } else {
-        // unit = span u: {offset, len} -> the unit record
+        // unit = span u of `len` bytes at `off`: make_unit(kWhole) restated in
+        // 32-bit arithmetic (everything but the address depends on p & 15 only;
+        // the generic form cost ~200 VALU per switch)
+        static_assert(kBlockBytes == 4096, "shifts below");
         const uint64_t off = a.offsets ? (uint64_t)__shfl(raw, g | 0, 64) | ((uint64_t)__shfl(raw, g | 1, 64) << 32)
                                        : u * a.stride;
         const bool sane = off <= a.base_bytes && a.len <= a.base_bytes - off;  // else: read nothing
-        const UnitRec r = make_unit(a.base, sane ? off : 0, sane ? a.len : 0u, 0u, sane, 0u, kWhole);
-        d.p = a.base + (r.a.x | ((uint64_t)r.a.y << 32));
-        d.eo = r.a.z;
-        d.nf = u < nunits ? r.b.z : 0u;  // flags 0: no unit
+        const uint32_t len = sane ? a.len : 0u;
+        const uint32_t kh = ((uint32_t)(uintptr_t)a.base + (uint32_t)off) & 15u;
+        const uint32_t vlen = len + ((0u - kh - len) & 15u);
+        const uint32_t x = vlen + kh;  // Ea - ph
+        const uint32_t g1o = x - kBlockBytes * ((x - 1) >> 12) - kh;  // span_head
+        const uint32_t po = len && g1o <= kFragMax ? g1o : 0u;
+        const uint32_t eo = vlen - po;
+        const uint32_t niters = len ? (eo + ((kh + po) & 15u) + kBlockBytes - 1) >> 12 : 0u;
+        d.p = a.base + (sane ? off : 0) + po;
+        d.eo = eo;
+        d.nf = u < nunits ? UnitDesc::kValid | UnitDesc::kSingle | (niters << 8) : 0u;  // flags 0: no unit
     }
     return d;
 }
