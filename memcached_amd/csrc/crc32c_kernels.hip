@@ -964,16 +964,6 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
     // the group's next block into `wn`.
     auto step = [&](BlockWin &w, BlockWin &wn) {
         const bool last = k + 1 >= cur.niters();
-        // a segment unit's shift row, loaded before this step's other loads:
-        // the multiply below waits for it alone, not for the block prefetch
-        // (under a wave-uniform branch: loads under divergent branches leave
-        // the waitcnt pass a merged state that drains the prefetch)
-        uint32_t segk = 0, fx1 = 0;
-        if (UNITS) {
-            segk = __shfl(cur.raw, (lane & 32u) | 7u, 64);
-            if (__builtin_amdgcn_readfirstlane(__any(last && !cur.single()))) fx1 = segpow_rows[32 * (segk & 255u) + li];
-            __builtin_amdgcn_sched_barrier(0);  // (issued before the block prefetch, not sunk after it)
-        }
         // next block: block k + 1 of cur, or block 0 of the unit in ring slot sl
         UnitDesc nd;
         if (__any(last)) {
@@ -982,6 +972,17 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
             nd = decode_unit<UNITS>(a, rw, u + ngroups_total, nunits, lane);
         }
         if (last && (li >> 3) == sl) ring = fetch_unit<UNITS>(a, u + 5 * ngroups_total, nunits, li);
+        // a segment unit's shift row, loaded after the (masked) ring refill and
+        // before the block prefetch: the multiply below then waits for exactly
+        // the block's loads issued after it, vmcnt(8), not for everything
+        // (under a wave-uniform branch: loads under divergent branches leave
+        // the waitcnt pass a merged state that drains the prefetch)
+        uint32_t segk = 0, fx1 = 0;
+        if (UNITS) {
+            segk = __shfl(cur.raw, (lane & 32u) | 7u, 64);
+            if (__builtin_amdgcn_readfirstlane(__any(last && !cur.single()))) fx1 = segpow_rows[32 * (segk & 255u) + li];
+            __builtin_amdgcn_sched_barrier(0);  // (issued before the block prefetch, not sunk after it)
+        }
         {
             UnitDesc t = cur;
             t.p = last ? nd.p : cur.p;
