@@ -1014,7 +1014,10 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
                 case 2: v = block_value<2>(w, c); break;
                 default: v = block_value<3>(w, c); break;
             }
-            acc = apply_op<4>(kAuxSpanFold, acc) ^ v;
+            // (the fold of a unit's first block is of acc = 0: skipped when no
+            // group of the wave is past its first block, e.g. one-block units)
+            if (__builtin_amdgcn_readfirstlane(__any(k != 0))) acc = apply_op<4>(kAuxSpanFold, acc);
+            acc ^= v;
         }
         if (last) {
             if (cur.valid()) {
