@@ -435,10 +435,10 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 // ===========================================================================
 //
 // Pieces as they lie.  A span D = [p, E) is read as the 16-B aligned pieces
-// [ph, Ea), ph = p rounded down and Ea = E rounded up to 16, foreign bytes
-// included: the span kernel computes R = raw([ph, Ea)) with no masking and no
-// initial value.  With F_h = [ph, p), F_t = [E, Ea), t = |F_t|, the algebra of
-// crc32c.c:58-137 gives
+// [ph, Ea), ph = p rounded down and Ea = E rounded up to 16 (tail_pad),
+// foreign bytes included: the span kernel computes R = raw([ph, Ea)) with no
+// masking and no initial value.  With F_h = [ph, p), F_t = [E, Ea),
+// t = |F_t|, the algebra of crc32c.c:58-137 gives
 //   raw([ph, Ea)) = M_{|D|+t}(raw(F_h)) ^ M_t(raw(D)) ^ raw(F_t), so
 //   crc32c(c, D) = ~M_{-t}(R ^ Z),   Z = M_{|D|+t}(~c ^ raw(F_h)) ^ raw(F_t).
 // Z depends only on c and the at most 30 foreign bytes, so one thread per
@@ -519,8 +519,14 @@ __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t *p) {
     return ld_u8(p) | (ld_u8(p + 1) << 8) | (ld_u8(p + 2) << 16) | (ld_u8(p + 3) << 24);
 }
 
+// t = Ea - E: a span's grid ends at Ea = E rounded up to 16.  (Rounding up to
+// a 128-B line makes every block whole lines -- a 16-B anchored block fetches
+// 33 lines per 4 KiB -- and the span kernel 1.6-2.4 % faster, but the span's
+// thread then reads and folds up to 127 foreign bytes: k_count +40 %, k_final
+// +57 %, a net loss on configs 2r and 5.)
+constexpr uint32_t kTailAlign = 16;
 __device__ __forceinline__ uint32_t tail_pad(const uint8_t *p, uint32_t len) {
-    return (uint32_t)(-(uintptr_t)(p + len)) & 15u;
+    return (uint32_t)(-(uintptr_t)(p + len)) & (kTailAlign - 1);
 }
 
 // Segments of a virtual span of vlen bytes, anchored at Ea; the head segment
@@ -530,8 +536,8 @@ __device__ __forceinline__ uint32_t nseg_of(uint32_t vlen) {
 }
 
 // Layout of the x^(8n) table (SpanArgs::xpow).
-constexpr uint32_t kXpowInv = 3072;  // x^(-8t), t < 16
-constexpr uint32_t kXpowL3 = 3088;   // x^(8 * 2^30 * j), j < 8
+constexpr uint32_t kXpowInv = 3072;                // x^(-8t), t < kTailAlign
+constexpr uint32_t kXpowL3 = kXpowInv + kTailAlign;  // x^(8 * 2^30 * j), j < 8
 constexpr uint32_t kXpowDwords = kXpowL3 + 8;
 
 // x^(8n) mod P (n < 2^33): one to four table entries multiplied.
@@ -648,8 +654,7 @@ __device__ __forceinline__ SpanHead span_head(const uint8_t *p, uint32_t len) {
 //   or, when G1 = Ea, Z = M_t(register from ~c over D);
 // - otherwise Z = M_{len+t}(~c ^ raw(F_h)) ^ raw(F_t): raw(F_h) = raw of the
 //   head piece's first kh bytes moved to its top (leading zeros leave a zero
-//   register unchanged), raw(F_t) = raw of the tail piece with its first
-//   16 - t bytes cleared.
+//   register unchanged), raw(F_t) = raw of the t bytes after E.
 // One thread.
 __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
                                               const uint32_t *xp) {
@@ -667,11 +672,7 @@ __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, ui
         if (kh) y ^= raw16(shl_bytes(ld_piece(p - kh), 16 - kh), t8);
         z = mulmodp_dev(y, xpow8_dev(xp, vlen));
     }
-    if (t) {
-        const Piece v = ld_piece(p + len + t - 16);
-        const Piece m = shl_bytes({~0ull, ~0ull}, 16 - t);
-        z ^= raw16({v.lo & m.lo, v.hi & m.hi}, t8);
-    }
+    if (t) z ^= reg_advance(0u, p + len, t, t8);  // raw(F_t)
     return z;
 }
 
@@ -807,8 +808,8 @@ __device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw,
                                        : u * a.stride;
         const bool sane = off <= a.base_bytes && a.len <= a.base_bytes - off;  // else: read nothing
         const uint32_t len = sane ? a.len : 0u;
-        const uint32_t kh = ((uint32_t)(uintptr_t)a.base + (uint32_t)off) & 15u;
-        const uint32_t vlen = len + ((0u - kh - len) & 15u);
+        const uint32_t plo = (uint32_t)(uintptr_t)a.base + (uint32_t)off, kh = plo & 15u;
+        const uint32_t vlen = len + ((0u - plo - len) & (kTailAlign - 1));  // tail_pad
         const uint32_t x = vlen + kh;  // Ea - ph
         const uint32_t g1o = x - kBlockBytes * ((x - 1) >> 12) - kh;  // span_head
         const uint32_t po = len && g1o <= kFragMax ? g1o : 0u;
@@ -1008,12 +1009,20 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
                                    : __all(grel + (int32_t)kRowBytes <= 0)     ? 1u
                                                                                : 0u;
             uint32_t v;
+#ifdef MCRC_ABL_LOADS_ONLY  // ablation: no chains (wrong CRCs): the loads and the per-unit work only
+            v = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v ^= w.v[r][0].x ^ w.v[r][0].y ^ w.v[r][0].z ^ w.v[r][0].w ^ w.v[r][1].x ^
+                                           w.v[r][1].y ^ w.v[r][1].z ^ w.v[r][1].w;
+            if (nskip == 7) v = 1;
+#else
             switch (nskip) {
                 case 0: v = block_value<0>(w, c); break;
                 case 1: v = block_value<1>(w, c); break;
                 case 2: v = block_value<2>(w, c); break;
                 default: v = block_value<3>(w, c); break;
             }
+#endif
             // (the fold of a unit's first block is of acc = 0: skipped when no
             // group of the wave is past its first block, e.g. one-block units)
             if (__builtin_amdgcn_readfirstlane(__any(k != 0))) acc = apply_op<4>(kAuxSpanFold, acc);

@@ -177,7 +177,7 @@ int init_device(Device &d, int id) {
         xp[1024 + j] = mcrc::xpow8n((uint64_t)j << 10);
         xp[2048 + j] = mcrc::xpow8n((uint64_t)j << 20);
     }
-    for (uint32_t t = 0; t < 16; ++t) xp[mcrc_dev::kXpowInv + t] = mcrc::xpow8n_inv(t);
+    for (uint32_t t = 0; t < mcrc_dev::kTailAlign; ++t) xp[mcrc_dev::kXpowInv + t] = mcrc::xpow8n_inv(t);
     for (uint32_t j = 0; j < 8; ++j) xp[mcrc_dev::kXpowL3 + j] = mcrc::xpow8n((uint64_t)j << 30);
     HIP_OK(hipMalloc(&d.img, img.size() * 4));
     HIP_OK(hipMemcpy(d.img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
@@ -302,8 +302,8 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     };
     const int g1 = (int)std::min<uint64_t>((n + 255) / 256, 4096);
     if (identity) {
-        // (spans of at most kFragMax - 15 bytes are all their threads' in k_final)
-        if (a.len + 15 > mcrc_dev::kFragMax) spans(a, grid_for(d, n));
+        // (spans of at most kFragMax - 127 bytes are all their threads' in k_final)
+        if (a.len + mcrc_dev::kTailAlign - 1 > mcrc_dev::kFragMax) spans(a, grid_for(d, n));
         hipLaunchKernelGGL((mcrc_dev::k_final<0, false>), dim3(g1), dim3(256), 0, st, a, nullptr);
         HIP_OK(hipGetLastError());
         return CRC32C_OK;

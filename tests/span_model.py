@@ -12,6 +12,7 @@ M32 = 0xFFFFFFFF
 
 
 def tail_pad(p, length):
+    """t = Ea - E, Ea = E rounded up to 16."""
     return (-(p + length)) & 15
 
 

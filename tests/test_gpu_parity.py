@@ -488,7 +488,8 @@ def test_offsets_with_fixed_length(torch):
     np.testing.assert_array_equal(outh, oracle.batch(host, offs, np.full(n, L)))
 
 
-@pytest.mark.parametrize("L", [1, 15, 100, 1008, 1009, 1010, 1024, 1040, 4080, 4097, 5104, 5125, 8195, 65536, 65552])
+@pytest.mark.parametrize("L", [1, 15, 100, 896, 897, 898, 1008, 1009, 1010, 1024, 1040, 4080, 4097, 5104, 5125, 8195,
+                               65536, 65552])
 def test_fixed_length_head_fragment_thresholds(torch, L):
     """offsets[] with one shared length (one unit per span, no plan) at the
     lengths where the head fragment moves between the span kernel and the
