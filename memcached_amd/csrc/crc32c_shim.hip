@@ -301,10 +301,14 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
                                mcrc_dev::kLdsImageK1Bytes, st, x, d.img);
     };
     const int g1 = (int)std::min<uint64_t>((n + 255) / 256, 4096);
+    // k_final: 1024 workgroups (it adds its bad count once per workgroup: 4096
+    // groups cost 30 us of same-address atomics per 4.8 M verified items, 64 Ki
+    // groups 190 us); k_count: 4096 (1024 measured 25 % slower on config 3).
+    const int gf = (int)std::min<uint64_t>((n + 255) / 256, 1024);
     if (identity) {
         // (spans of at most kFragMax - 127 bytes are all their threads' in k_final)
         if (a.len + mcrc_dev::kTailAlign - 1 > mcrc_dev::kFragMax) spans(a, grid_for(d, n));
-        hipLaunchKernelGGL((mcrc_dev::k_final<0, false>), dim3(g1), dim3(256), 0, st, a, nullptr);
+        hipLaunchKernelGGL((mcrc_dev::k_final<0, false>), dim3(gf), dim3(256), 0, st, a, nullptr);
         HIP_OK(hipGetLastError());
         return CRC32C_OK;
     }
@@ -335,7 +339,7 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     w.units = d.whole;
     w.nunits = nwhole;
     spans(w, d.cus);
-    hipLaunchKernelGGL((mcrc_dev::k_final<MODE, true>), dim3(g1), dim3(256), 0, st, u, d.irec);
+    hipLaunchKernelGGL((mcrc_dev::k_final<MODE, true>), dim3(gf), dim3(256), 0, st, u, d.irec);
     HIP_OK(hipGetLastError());
     return CRC32C_OK;
 }
