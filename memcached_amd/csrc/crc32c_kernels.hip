@@ -497,7 +497,7 @@ struct SpanArgs {
     uint64_t n;                // spans (items)
     const uint32_t *xpow;      // x^(8*j), x^(8*1024*j), x^(8*2^20*j) (3 x 1024), x^(-8t) (16),
                                // x^(8*2^30*j) (8): layout kXpow*
-    const uint32_t *tab8;      // 4 x 256 byte tables (Tab8)
+    const uint32_t *tab8;      // 16 x 256 byte tables (Tab8)
     const uint4 *zero;         // kZeroBytes of zeros in device memory
     // work units (nullptr: unit u = span u, one segment)
     const struct UnitRec *units;
@@ -564,20 +564,37 @@ __device__ __forceinline__ Piece shl_bytes(Piece v, uint32_t s) {
     if (s == 0) return v;
     return {v.lo << (8 * s), (v.hi << (8 * s)) | (v.lo >> (64 - 8 * s))};
 }
-// Byte tables in LDS for the per-thread work of k_count / k_final: [0] is
-// crc32c.c:399's byte-wise table (crc32c_table_little[0]), [k] the same
-// followed by k zero bytes, so a dword is one slice-by-4 step (crc32c.c:401-415's
-// form).  (A copy per bank, conflict-free but four dependent lookups per dword,
-// measured slower: the per-thread chains are latency-bound.)
+// Byte tables in LDS for the per-thread work of k_count / k_final: T_j[b] =
+// the register after byte b followed by j zero bytes, j < 16 (T_0 is
+// crc32c.c:399's byte-wise table crc32c_table_little[0]; crc32c.c:401-415 uses
+// eight of them).  A whole 16-B piece is one step of 16 independent lookups:
+// only the four that read the running register depend on the previous step,
+// so a thread's chain is one LDS latency per 16 bytes.  (A dword per step
+// took 0.21 ms of k_count on config 3, a copy of one table per bank with four
+// dependent lookups per dword 0.45 ms: the per-thread chains are
+// latency-bound, not conflict-bound.)
 struct Tab8 {
-    const uint32_t *s;
-    __device__ __forceinline__ uint32_t step(uint32_t r) const { return s[r & 255u] ^ (r >> 8); }
-    __device__ __forceinline__ uint32_t dword(uint32_t r, uint32_t d) const {
-        r ^= d;
-        return s[768 + (r & 255u)] ^ s[512 + ((r >> 8) & 255u)] ^ s[256 + ((r >> 16) & 255u)] ^ s[r >> 24];
+    const uint32_t *s;  // T_j at s + 256 j
+    __device__ __forceinline__ uint32_t T(uint32_t j, uint32_t b) const { return s[256 * j + b]; }
+    // the register r advanced over the 16 bytes of v
+    __device__ __forceinline__ uint32_t piece(uint32_t r, Piece v) const {
+        const uint32_t x = r ^ (uint32_t)v.lo, d1 = (uint32_t)(v.lo >> 32), d2 = (uint32_t)v.hi,
+                       d3 = (uint32_t)(v.hi >> 32);
+        return (T(15, x & 255u) ^ T(14, (x >> 8) & 255u) ^ T(13, (x >> 16) & 255u) ^ T(12, x >> 24)) ^
+               (T(11, d1 & 255u) ^ T(10, (d1 >> 8) & 255u) ^ T(9, (d1 >> 16) & 255u) ^ T(8, d1 >> 24)) ^
+               (T(7, d2 & 255u) ^ T(6, (d2 >> 8) & 255u) ^ T(5, (d2 >> 16) & 255u) ^ T(4, d2 >> 24)) ^
+               (T(3, d3 & 255u) ^ T(2, (d3 >> 8) & 255u) ^ T(1, (d3 >> 16) & 255u) ^ T(0, d3 >> 24));
+    }
+    // M_n(r): the register r advanced over n zero bytes, 1 <= n <= 16
+    __device__ __forceinline__ uint32_t zeros(uint32_t r, uint32_t n) const {
+        if (n >= 4)
+            return T(n - 1, r & 255u) ^ T(n - 2, (r >> 8) & 255u) ^ T(n - 3, (r >> 16) & 255u) ^ T(n - 4, r >> 24);
+        uint32_t z = n == 0 ? r : r >> (8 * n);  // the bytes not yet shifted out
+        for (uint32_t k = 0; k < n; ++k) z ^= T(n - 1 - k, (r >> (8 * k)) & 255u);
+        return z;
     }
 };
-constexpr uint32_t kTab8Dwords = 4 * 256;
+constexpr uint32_t kTab8Dwords = 16 * 256;  // 16 KiB
 // (every thread of the block calls it)
 __device__ __forceinline__ Tab8 load_tab8(uint32_t *s, const uint32_t *tab8) {
     for (uint32_t i = threadIdx.x; i < kTab8Dwords; i += blockDim.x) s[i] = tab8[i];
@@ -586,41 +603,35 @@ __device__ __forceinline__ Tab8 load_tab8(uint32_t *s, const uint32_t *tab8) {
 }
 
 // Register after the 16 bytes of v from a zero register.
-__device__ __forceinline__ uint32_t raw16(Piece v, const Tab8 &t) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r = t.dword(r, (uint32_t)((k < 2 ? v.lo : v.hi) >> (32 * (k & 1))));
-    return r;
+__device__ __forceinline__ uint32_t raw16(Piece v, const Tab8 &t) { return t.piece(0u, v); }
+
+// Bytes [0, k) of v cleared.
+__device__ __forceinline__ Piece clear_below(Piece v, uint32_t k) {
+    const Piece m = shl_bytes({~0ull, ~0ull}, k);
+    return {v.lo & m.lo, v.hi & m.hi};
 }
 
-// Byte b (dynamic, < 16) of a piece.
-__device__ __forceinline__ uint32_t byte_of(Piece v, uint32_t b) {
-    return (uint32_t)(b < 8 ? v.lo >> (8 * b) : v.hi >> (8 * (b - 8))) & 255u;
-}
-// Register r advanced over the n bytes at p (one thread): the partial first
-// and last 16-B pieces byte by byte, whole pieces dword by dword.  Every
-// load is an aligned piece holding a byte of [p, p + n).
+// Register r advanced over the n bytes at p (one thread), one step per 16-B
+// piece: a partial first or last piece is moved to the top of a zeroed piece
+// (leading zeros leave a zero register unchanged), so
+//   r' = M_m(r) ^ raw16(the m bytes at the top).
+// Every load is an aligned piece holding a byte of [p, p + n).
 __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, uint32_t n, const Tab8 &t) {
     if (n == 0) return r;
     const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
     const uint8_t *q = p - kh;
-    Piece v = ld_piece(q);
-    const uint32_t b1 = kh + n < 16u ? kh + n : 16u;
-    for (uint32_t b = kh; b < b1; ++b) r = t.step(r ^ byte_of(v, b));
-    n -= b1 - kh;
-    q += 16;
-#pragma unroll 8
-    for (; n >= 16; n -= 16, q += 16) {
-        v = ld_piece(q);
-        r = t.dword(r, (uint32_t)v.lo);
-        r = t.dword(r, (uint32_t)(v.lo >> 32));
-        r = t.dword(r, (uint32_t)v.hi);
-        r = t.dword(r, (uint32_t)(v.hi >> 32));
+    if (kh + n <= 16u) {  // inside one piece: bytes [kh, kh + n)
+        const Piece v = shl_bytes(ld_piece(q), 16u - kh - n);
+        return t.zeros(r, n) ^ raw16(clear_below(v, 16u - n), t);
     }
-    if (n) {
-        v = ld_piece(q);
-        for (uint32_t b = 0; b < n; ++b) r = t.step(r ^ byte_of(v, b));
+    if (kh) {  // bytes [kh, 16) of the first piece
+        r = t.zeros(r, 16u - kh) ^ raw16(clear_below(ld_piece(q), kh), t);
+        n -= 16u - kh;
+        q += 16;
     }
+#pragma unroll 4
+    for (; n >= 16; n -= 16, q += 16) r = t.piece(r, ld_piece(q));
+    if (n) r = t.zeros(r, n) ^ raw16(shl_bytes(ld_piece(q), 16u - n), t);  // bytes [0, n) of the last piece
     return r;
 }
 

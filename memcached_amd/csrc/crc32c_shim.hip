@@ -165,9 +165,9 @@ int init_device(Device &d, int id) {
     d.cus = p.multiProcessorCount;
     std::vector<uint32_t> img(mcrc::kImageK1Dwords);
     mcrc::build_lds_image_span(img.data(), mcrc_dev::kSpanCH);
-    std::vector<uint32_t> tab8(1024);  // [k][b]: the byte-wise table followed by k zero bytes
+    std::vector<uint32_t> tab8(mcrc_dev::kTab8Dwords);  // [k][b]: the byte-wise table followed by k zero bytes
     mcrc::build_t0(tab8.data());
-    for (uint32_t k = 1; k < 4; ++k) {
+    for (uint32_t k = 1; k < mcrc_dev::kTab8Dwords / 256; ++k) {
         const mcrc::Gf2Op zk = mcrc::Gf2Op::zeros(k);
         for (uint32_t b = 0; b < 256; ++b) tab8[256 * k + b] = zk.apply(tab8[b]);
     }
