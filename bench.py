@@ -246,6 +246,9 @@ def run_verify_steps(args_v, steps: int, stream):
     return evs, int(nbad.value)
 
 
+_KEEP = []  # device tensors whose raw pointers a workload hands to the library
+
+
 def workload_config5(args, rank, world):
     """Extstore pages of packed 4165-byte item images, stored CRCs verified (K3).
 
@@ -295,6 +298,7 @@ def workload_config5(args, rank, world):
     flat[pos] ^= (torch.ones_like(bit) << bit)
     ok = torch.empty(n, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
+    _KEEP.extend((data, offs))  # the raw pointers below must outlive this frame
     return (data.data_ptr(), data.numel(), wbuf, offs.data_ptr(), n, ok.data_ptr()), ok, victims, \
         n * (ntotal - 32), {
             "workload": f"BASELINE configs[4]: {args.pages} x 64 MiB extstore pages, 16 wbufs x 1007 packed "
@@ -334,7 +338,7 @@ def main():
     ap.add_argument("--fill", default="splitmix", choices=["splitmix", "randint"],
                     help="item bytes: splitmix64(42 + rank) words (SURVEY.md 8d) or torch.randint")
     ap.add_argument("--workload", default="config2",
-                    choices=["config2", "config2r", "config3", "config5", "pages", "stamp", "host"],
+                    choices=["config2", "config2r", "config3", "config5", "pages", "stamp", "host", "calls"],
                     help="config2 = headline; others are extra measurements (not the bench line)")
     ap.add_argument("--pages", type=int, default=1000, help="config5: 64 MiB pages per GPU")
     ap.add_argument("--span-len", type=int, default=4133, help="config2r: span length (stride = len + 32)")
@@ -484,6 +488,44 @@ def extra_workload(args):
         res.update(config=cfg, kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
                    hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), nbad=int(nbad.value),
                    nitems=int(nitems.value) if args.workload == "pages" else n, items_written=n)
+    elif args.workload == "calls":
+        # Per-call latency of the integration's call shapes (INTEGRATION.md
+        # 2-4): wall clock of synchronous calls, launch and sync included.
+        import time
+
+        import numpy as np
+        args.pages = 1
+        vargs, ok, victims, nbytes, cfg = workload_config5(args, rank, world)
+        base, size, region, offs, n, okp = vargs
+        nbad = ctypes.c_uint64(0)
+        per_wbuf = 1007
+        torch.cuda.synchronize()
+
+        def per_call(fn, reps):
+            fn()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / reps * 1e6
+
+        sptr = ctypes.c_void_p(stream.cuda_stream)
+        stamp_us = per_call(lambda: _lib.check(_lib.lib.crc32c_stamp_items(
+            base, region, region, offs, per_wbuf, None, ctypes.byref(nbad), _lib.CRC32C_DEVICE, sptr)), 200)
+        verify64_us = per_call(lambda: _lib.check(_lib.lib.crc32c_verify_items(
+            base, region, region, offs, 64, okp, ctypes.byref(nbad), _lib.CRC32C_DEVICE, sptr)), 200)
+        host = np.frombuffer(bytearray(64 * 4165 + 64), dtype=np.uint8)
+        hoffs = (np.arange(64, dtype=np.uint64) * 4165 + 32).astype(np.uint64)
+        hout = np.empty(64, np.uint32)
+        hs = _lib.Spans(host.ctypes.data, host.size, hoffs.ctypes.data, 0, None, 4133, None, hout.ctypes.data, 64)
+        host64_us = per_call(lambda: _lib.check(_lib.lib.crc32c_batch(ctypes.byref(hs), 0, None)), 200)
+        res.update(config={"workload": "per-call latency, synchronous calls: stamp one 4 MiB wbuf of 1007 images "
+                                       "(device), verify an IO batch of 64 images (device), CRC 64 x 4133-B "
+                                       "spans in pageable host memory (host path)"},
+                   stamp_wbuf_us=round(stamp_us, 1), verify64_us=round(verify64_us, 1),
+                   host_batch64_us=round(host64_us, 1),
+                   stamp_wbuf_gb_s=round(per_wbuf * 4133 / (stamp_us * 1e-6) / 1e9, 1))
     else:  # host: pinned host memory -> H2D -> K1/K2 -> D2H through the library's host path
         import numpy as np
         n = args.items

@@ -1237,6 +1237,85 @@ __global__ void k_final(SpanArgs a, const uint4 *irec) {
     count_bad(a.nbad, nb);
 }
 
+// Small batches: one launch.  Up to kSmallMax spans, one 32-lane group per
+// span, 32 spans per workgroup: the group reads the whole span [ph, Ea) in
+// 4 KiB blocks anchored at Ea (no plan, no segments, no head fragment), reduces
+// it to R, and its lanes compute Z from the span image's own tables
+// (raw16 by dword steps, the x^(8n) multiplies) and emit.  The planned path's
+// seven launches (count, scan, expand, span kernel x 2, final) cost ~80 us per
+// call whatever the batch; a storage.c wbuf stamp (1007 images) or an IO-batch
+// verify is one call of this kernel.
+constexpr uint32_t kSmallMax = 8192;
+
+// Register after the 16 bytes of v from a zero register, on the span image's
+// replicated slice-by-4 tables (this lane's copy).
+__device__ __forceinline__ uint32_t raw16_img(Piece v, const LaneCtx &c) {
+    uint32_t x = (uint32_t)v.lo;
+    x = step4_next(x, (uint32_t)(v.lo >> 32), c);
+    x = step4_next(x, (uint32_t)v.hi, c);
+    x = step4_next(x, (uint32_t)(v.hi >> 32), c);
+    return step4_next(x, 0u, c);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_small(SpanArgs a, const uint4 *__restrict__ img) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    load_tables(smem, img, kLdsImageK1Bytes);
+    const uint32_t lane = threadIdx.x & 63u, li = lane & 31u;
+    LaneCtx c;
+    c.lane4 = li << 2;
+    c.lane4hi = c.lane4 | 0x10000u;
+    const uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5);
+    const bool valid = i < a.n;
+    ItemDesc it{a.base, 0u, 0u, false};
+    if (valid) it = fetch_item<MODE>(a, i);
+    const uint32_t len = it.sane ? it.len : 0u;
+    const uint32_t t = tail_pad(it.p, len), eo = len + t;
+    const uint32_t niters = len ? (eo + (uint32_t)((uintptr_t)it.p & 15u) + kBlockBytes - 1) / kBlockBytes : 0u;
+    const uint32_t nmax = __builtin_amdgcn_readfirstlane(max(niters, (uint32_t)__shfl_xor(niters, 32, 64)));
+    const uint4 *zero = a.zero + (blockIdx.x % kZeroSlots) * (4096 / 16);
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < nmax; ++k) {
+        UnitDesc d;
+        d.p = it.p;
+        d.eo = eo;
+        d.nf = k < niters ? (niters << 8) | UnitDesc::kValid : 0u;  // (a finished group reads zeros)
+        d.raw = 0;
+        BlockWin w;
+        load_block(w, d, k, li, zero);
+        const uint32_t v = block_value<0>(w, c);
+        if (k < niters) acc = apply_op<4>(kAuxSpanFold, acc) ^ v;
+    }
+    const uint32_t R = group_reduce32_span(acc, lane);
+    uint32_t nb = 0;
+    if (valid) {
+        // Z (span_corr, no fragment): M_{len+t}(~c ^ raw(F_h)) ^ raw(F_t)
+        const uint32_t cin = MODE == 0 ? it.aux : 0u;
+        uint32_t z = mulmodp_dev(~cin, a.xpow[t]);  // (len 0: R = 0, crc = c)
+        if (len) {
+            const uint32_t kh = (uint32_t)((uintptr_t)it.p & 15u);
+            uint32_t y = ~cin;
+            if (kh) y ^= raw16_img(shl_bytes(ld_piece(it.p - kh), 16 - kh), c);
+            z = mulmodp_dev(y, xpow8_dev(a.xpow, (uint64_t)len + t));
+            if (t) z ^= raw16_img(clear_below(ld_piece(it.p + len + t - 16), 16 - t), c);
+        }
+        if (MODE == 1) {
+            const bool good = it.sane && R == (z ^ mulmodp_dev(~it.aux, a.xpow[t]));
+            if (li == 0) a.ok[i] = good;
+            nb = li == 0 && !good;
+        } else {
+            uint32_t v = R ^ z;
+            if (t) v = mulmodp_dev(v, a.xpow[kXpowInv + t]);
+            if (li == 0) emit<MODE>(a, i, ~v, it.sane, it.p);
+            nb = li == 0 && !it.sane;
+        }
+    }
+    // one atomic per wave with a bad span (all 160 KiB of LDS hold the tables,
+    // so no workgroup-level sum as in count_bad)
+    const uint64_t m = __ballot(nb != 0);
+    if (m && lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) atomicAdd(a.nbad, (unsigned long long)__popcll(m));
+}
+
 // Chained CRC over an iov list (the chunked-item read verify of
 // storage.c:163-170: crc = crc32c(0, iov0 + 32, ...), then
 // crc = crc32c(crc, iov_x) for every chunk).  Given crc_i = crc32c(0, iov_i),

@@ -219,6 +219,9 @@ int init_device(Device &d, int id) {
     const void *spans[] = {
         (const void *)mcrc_dev::k_spans<false>,
         (const void *)mcrc_dev::k_spans<true>,
+        (const void *)mcrc_dev::k_small<0>,
+        (const void *)mcrc_dev::k_small<1>,
+        (const void *)mcrc_dev::k_small<2>,
     };
     for (const void *k : spans)
         HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImageK1Bytes));
@@ -287,6 +290,14 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
     return CRC32C_OK;
 }
 
+// Batches of at most this many spans take the single-launch k_small.
+// MCRC_SMALL_MAX in the environment overrides it (read per call; the parity
+// tests run every case through both paths with 0 and the default).
+uint64_t small_max() {
+    const char *e = getenv("MCRC_SMALL_MAX");
+    return e ? std::min<uint64_t>(strtoull(e, nullptr, 10), mcrc_dev::kSmallMax) : mcrc_dev::kSmallMax;
+}
+
 template <int MODE>
 int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) {
     const uint64_t n = a.n;
@@ -305,6 +316,12 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     // groups cost 30 us of same-address atomics per 4.8 M verified items, 64 Ki
     // groups 190 us); k_count: 4096 (1024 measured 25 % slower on config 3).
     const int gf = (int)std::min<uint64_t>((n + 255) / 256, 1024);
+    if (n <= small_max()) {  // one launch (k_small)
+        hipLaunchKernelGGL((mcrc_dev::k_small<MODE>), dim3((unsigned)((n + 31) / 32)), dim3(1024),
+                           mcrc_dev::kLdsImageK1Bytes, st, a, d.img);
+        HIP_OK(hipGetLastError());
+        return CRC32C_OK;
+    }
     if (identity) {
         // (spans of at most kFragMax - 127 bytes are all their threads' in k_final)
         if (a.len + mcrc_dev::kTailAlign - 1 > mcrc_dev::kFragMax) spans(a, grid_for(d, n));

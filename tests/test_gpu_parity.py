@@ -19,6 +19,18 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+@pytest.fixture(autouse=True, params=["small", "planned"])
+def span_path(request, monkeypatch):
+    """Every case runs twice: batches of at most 8192 spans through the
+    single-launch k_small (the default) and through the planned path
+    (count / scan / expand / span kernel / final) that larger batches take."""
+    if request.param == "planned":
+        monkeypatch.setenv("MCRC_SMALL_MAX", "0")
+    else:
+        monkeypatch.delenv("MCRC_SMALL_MAX", raising=False)
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def torch():
     import torch as t
