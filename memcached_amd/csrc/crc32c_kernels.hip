@@ -1275,16 +1275,27 @@ __global__ __launch_bounds__(1024) void k_small(SpanArgs a, const uint4 *__restr
     const uint32_t nmax = __builtin_amdgcn_readfirstlane(max(niters, (uint32_t)__shfl_xor(niters, 32, 64)));
     const uint4 *zero = a.zero + (blockIdx.x % kZeroSlots) * (4096 / 16);
     uint32_t acc = 0;
-    for (uint32_t k = 0; k < nmax; ++k) {
+    // block k + 1 is loaded before block k is reduced (two register sets)
+    auto issue = [&](BlockWin &w, uint32_t k) {
         UnitDesc d;
         d.p = it.p;
         d.eo = eo;
-        d.nf = k < niters ? (niters << 8) | UnitDesc::kValid : 0u;  // (a finished group reads zeros)
+        d.nf = k < niters ? (niters << 8) | UnitDesc::kValid : 0u;  // (past the span: zeros)
         d.raw = 0;
-        BlockWin w;
         load_block(w, d, k, li, zero);
+    };
+    auto reduce = [&](const BlockWin &w, uint32_t k) {
         const uint32_t v = block_value<0>(w, c);
         if (k < niters) acc = apply_op<4>(kAuxSpanFold, acc) ^ v;
+    };
+    BlockWin w0, w1;
+    if (nmax) issue(w0, 0);
+    for (uint32_t k = 0; k < nmax; k += 2) {
+        issue(w1, k + 1);
+        reduce(w0, k);
+        if (k + 1 >= nmax) break;
+        issue(w0, k + 2);
+        reduce(w1, k + 1);
     }
     const uint32_t R = group_reduce32_span(acc, lane);
     uint32_t nb = 0;

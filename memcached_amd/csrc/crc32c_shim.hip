@@ -72,6 +72,7 @@ struct Device {
     uint32_t *xpow = nullptr;   // x^(8n) table (layout mcrc_dev::kXpow*)
     uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
     unsigned long long *nbad = nullptr;
+    unsigned long long *hbad = nullptr;  // pinned twin of nbad (a D2H copy into pageable memory is a slow path)
     hipStream_t stream = nullptr, copy = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};  // host-batch pipeline slots
@@ -203,6 +204,7 @@ int init_device(Device &d, int id) {
     HIP_OK(hipMalloc(&d.zero, mcrc_dev::kZeroBytes));
     HIP_OK(hipMemset(d.zero, 0, mcrc_dev::kZeroBytes));
     HIP_OK(hipMalloc(&d.nbad, sizeof(unsigned long long)));
+    HIP_OK(hipHostMalloc(&d.hbad, sizeof(unsigned long long), hipHostMallocDefault));
     HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&d.ev0));
@@ -293,6 +295,8 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
 // Batches of at most this many spans take the single-launch k_small.
 // MCRC_SMALL_MAX in the environment overrides it (read per call; the parity
 // tests run every case through both paths with 0 and the default).
+constexpr uint64_t kSmallSpanMax = 1 << 20;   // fixed-length batches: spans up to 1 MiB
+constexpr uint64_t kSmallBaseMax = 8ull << 20;  // else: a buffer of at most 8 MiB (a wbuf, an IO batch)
 uint64_t small_max() {
     const char *e = getenv("MCRC_SMALL_MAX");
     return e ? std::min<uint64_t>(strtoull(e, nullptr, 10), mcrc_dev::kSmallMax) : mcrc_dev::kSmallMax;
@@ -316,7 +320,11 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     // groups cost 30 us of same-address atomics per 4.8 M verified items, 64 Ki
     // groups 190 us); k_count: 4096 (1024 measured 25 % slower on config 3).
     const int gf = (int)std::min<uint64_t>((n + 255) / 256, 1024);
-    if (n <= small_max()) {  // one launch (k_small)
+    // One launch (k_small) for small batches whose spans are bounded: a group
+    // reads its whole span alone, so a batch of a few multi-MiB spans is
+    // left to the planned path (segments over the whole grid).
+    const bool bounded = MODE == 0 && a.lens == nullptr ? a.len <= kSmallSpanMax : a.base_bytes <= kSmallBaseMax;
+    if (n <= small_max() && bounded) {
         hipLaunchKernelGGL((mcrc_dev::k_small<MODE>), dim3((unsigned)((n + 31) / 32)), dim3(1024),
                            mcrc_dev::kLdsImageK1Bytes, st, a, d.img);
         HIP_OK(hipGetLastError());
@@ -651,7 +659,7 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
     unsigned long long bad = 0;
     std::vector<uint32_t> crcs;
     std::vector<uint8_t> oks;
-    bool fail = hipMemcpyAsync(&bad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st) != hipSuccess;
+    bool fail = hipMemcpyAsync(d->hbad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st) != hipSuccess;
     if (!dev && MODE == 1) fail = fail || hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, st) != hipSuccess;
     if (!dev && MODE == 2) {
         crcs.resize(n);
@@ -662,6 +670,7 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
     fail = fail || hipStreamSynchronize(st) != hipSuccess;
     cleanup();
     if (fail) return CRC32C_EHIP;
+    bad = *d->hbad;
     if (!dev && MODE == 2) {
         uint8_t *b = (uint8_t *)base;
         for (uint64_t i = 0; i < n; ++i)
@@ -741,10 +750,13 @@ int crc32c_batch(const crc32c_spans *s, unsigned flags, void *stream) {
     // spans given by offsets / lengths are range-checked on the device
     unsigned long long nrange = 0;
     const bool checked = s->n && (s->offsets || s->lens);
-    if (checked) HIP_OK(hipMemcpyAsync(&nrange, d->nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
+    if (checked) HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
     d->release(st);
     HIP_OK(hipEventSynchronize(d->ev1));
-    if (checked) HIP_OK(hipStreamSynchronize(st));
+    if (checked) {
+        HIP_OK(hipStreamSynchronize(st));
+        nrange = *d->hbad;
+    }
     (void)hipEventElapsedTime(&g_last_kernel_ms, d->ev0, d->ev1);
     return nrange ? CRC32C_ERANGE : CRC32C_OK;
 }
@@ -775,12 +787,15 @@ int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, u
     const uint64_t *first = chain_first;
     uint32_t *dout = out;
     unsigned long long nrange = 0;
+    bool nrange_copied = false;
     if (dev) {
         if (!device_range_ok(iovs->base, iovs->base_bytes)) return CRC32C_EINVAL;
         rc = enqueue_device(*d, *iovs, flags, st);
         if (rc) return rc;
-        if (!(flags & CRC32C_ASYNC) && (iovs->offsets || iovs->lens))  // range-checked on the device
-            HIP_OK(hipMemcpyAsync(&nrange, d->nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
+        if (!(flags & CRC32C_ASYNC) && (iovs->offsets || iovs->lens)) {  // range-checked on the device
+            HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
+            nrange_copied = true;
+        }
     } else {  // stage the fold's inputs (small: 4-8 B per iov / chain)
         const uint64_t n = iovs->n;
         uint8_t *buf = (uint8_t *)d->grow(kScrStage, n * 8 + (nchains + 1) * 8 + nchains * 4 + 64);
@@ -802,6 +817,7 @@ int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, u
     HIP_OK(hipGetLastError());
     if (!dev) HIP_OK(hipMemcpyAsync(out, dout, nchains * 4, hipMemcpyDeviceToHost, st));
     if (!dev || !(flags & CRC32C_ASYNC)) HIP_OK(hipStreamSynchronize(st));
+    if (nrange_copied) nrange = *d->hbad;
     return nrange ? CRC32C_ERANGE : CRC32C_OK;
 }
 
@@ -898,8 +914,7 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     HIP_OK(hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st));
     rc = launch_units<1>(*d, a, false, st);
     if (rc) return rc;
-    unsigned long long bad = 0;
-    HIP_OK(hipMemcpyAsync(&bad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     const uint64_t k = std::min<uint64_t>(cap, total);
     if (!direct && k) {
         const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -907,7 +922,7 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
         HIP_OK(hipMemcpyAsync(ok, dok, k, kind, st));
     }
     HIP_OK(hipStreamSynchronize(st));
-    *nbad = bad;
+    *nbad = *d->hbad;
     return CRC32C_OK;
 }
 
