@@ -7,4 +7,5 @@ run 600 python bench.py --workload config2r --steps 10 --warmup 2 > $O/config2r.
 run 600 python bench.py --workload pages --pages ${PAGES:-1000} --steps 3 --warmup 1 > $O/pages.json 2> $O/pages.err
 run 600 python bench.py --workload stamp --pages ${PAGES:-1000} --steps 3 --warmup 1 > $O/stamp.json 2> $O/stamp.err
 run 600 python bench.py --workload host --steps 5 --warmup 1 > $O/host.json 2> $O/host.err
+run 600 python bench.py --workload calls > $O/calls.json 2> $O/calls.err
 echo done
