@@ -942,13 +942,16 @@ constexpr uint32_t kSpanBlock = MCRC_SPAN_BLOCK;
 template <bool UNITS>
 __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *__restrict__ img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint64_t nunits = UNITS ? (uint64_t)*a.nunits : a.n;
+    // a workgroup without a unit leaves before loading 160 KiB of tables (the
+    // overlap pass is usually empty, and small plans do not fill the grid)
+    if ((uint64_t)blockIdx.x * (blockDim.x >> 5) >= nunits) return;
     load_tables(smem, img, kLdsImageK1Bytes);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t li = lane & 31u;
     LaneCtx c;
     c.lane4 = li << 2;
     c.lane4hi = c.lane4 | 0x10000u;
-    const uint64_t nunits = UNITS ? (uint64_t)*a.nunits : a.n;
     const uint64_t ngroups_total = (uint64_t)gridDim.x * (blockDim.x >> 5);
     uint64_t u = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
 
