@@ -657,6 +657,19 @@ __device__ __forceinline__ SpanHead span_head(const uint8_t *p, uint32_t len) {
     return {g1o, len != 0 && g1o <= kFragMax};
 }
 
+// One-block geometry of span [p, p + len): true (and G1) if its unit is one
+// whole block at G1 = p + g1o, or it has no unit at all (false: neither).
+__device__ __forceinline__ bool one_block(const uint8_t *p, uint32_t len, const uint8_t **g1, bool *none) {
+    const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
+    const uint32_t vlen = len + tail_pad(p, len);
+    const uint32_t x = vlen + kh;  // Ea - ph
+    const uint32_t g1o = x - kBlockBytes * ((x - 1) / kBlockBytes) - kh;
+    const bool drop = len != 0 && g1o <= kFragMax;
+    *none = len == 0 || (drop && g1o == vlen);
+    *g1 = p + g1o;
+    return *none || (drop && vlen - g1o == kBlockBytes);
+}
+
 // Z of span [p, p + len) with initial CRC c (see "Pieces as they lie"), for
 // the R that the span kernel computes over the span's units:
 // - no bytes: the kernel reads nothing (R = 0), Z = M_t(~c);
@@ -1104,14 +1117,19 @@ __device__ __forceinline__ uint32_t span_units(const uint8_t *p, uint32_t len) {
 // the foreign bytes of the head and tail pieces are read here: for packed
 // images they share lines with the headers this pass reads anyway).
 template <int MODE>
-__global__ void k_count(SpanArgs a, uint32_t *nunit, uint4 *irec) {
+__global__ void k_count(SpanArgs a, uint32_t *nunit, uint4 *irec, uint8_t *fast) {
     __shared__ uint32_t s8[kTab8Dwords];
     const Tab8 t8 = load_tab8(s8, a.tab8);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x)
     {
         const ItemDesc it = fetch_item<MODE>(a, i);
-        nunit[i] = span_units(it.p, it.len);
+        // a span whose unit is one whole block goes to k_blocks (no units)
+        const uint8_t *g1;
+        bool none;
+        const bool one = it.sane && one_block(it.p, it.len, &g1, &none) && !none;
+        fast[i] = one;
+        nunit[i] = one ? 0u : span_units(it.p, it.len);
         const uint64_t off = (uint64_t)(it.p - a.base);
         uint32_t z = 0;
         if (it.sane) {
@@ -1328,6 +1346,140 @@ __global__ __launch_bounds__(1024) void k_small(SpanArgs a, const uint4 *__restr
     // so no workgroup-level sum as in count_bad)
     const uint64_t m = __ballot(nb != 0);
     if (m && lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) atomicAdd(a.nbad, (unsigned long long)__popcll(m));
+}
+
+// ===========================================================================
+// K4: one-block units (K1's loop over gathered blocks)
+// ===========================================================================
+//
+// A span whose unit is exactly one 4 KiB block starting on its grid (its head
+// fragment went to its thread: every 4133-B item of configs 2r and 5) needs
+// none of the span kernel's unit machinery.  k_blocks runs K1's loop (MODE
+// 14: four steps reduced by one tree, no row folds) over those blocks, with
+// each group's block address gathered per span instead of base + i * stride,
+// and writes R (no initial value, no final XOR): out[i] without a plan,
+// span_acc[i] with one.  A span's descriptor is loaded two steps before its
+// block: vmcnt counts in issue order, so when the address is needed only the
+// newer block loads may still be pending.
+struct BlkRegs {
+    ItemRegs<32, 32, 4> d;
+    uint4 rec;      // descriptor of the block this buffer loads next
+    uint32_t rs;    // (planned) its span
+    uint32_t sidx;  // (planned) the span of the block two loads later
+    uint32_t cur;   // (planned) the span of the block in d
+};
+
+template <bool IDENT, bool OFFS>
+__global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__restrict__ img, const uint4 *irec,
+                                                 const uint32_t *fastidx, const uint32_t *nfast) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // without a plan block j is span j; with one, span fastidx[j] of the nfast
+    // spans k_count found to be one block
+    const uint64_t n = IDENT ? a.n : (uint64_t)*nfast;
+    const uint64_t waves = blockDim.x >> 6;
+    const uint64_t gstep = gridDim.x * waves;
+    const uint64_t ngroups = (n + 1) / 2;
+    uint64_t grp = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
+    if ((uint64_t)blockIdx.x * waves >= ngroups) return;
+    load_tables(smem, img, kLdsImageK1Bytes);
+    if (grp >= ngroups) return;
+    const uint32_t lane = threadIdx.x & 63u, li = lane & 31u, g = lane >> 5;
+    LaneCtx c;
+    c.lane4 = li << 2;
+    c.lane4hi = c.lane4 | 0x10000u;
+    const uint8_t *zero = reinterpret_cast<const uint8_t *>(a.zero + (blockIdx.x % kZeroSlots) * (4096 / 16));
+    auto item_of = [&](uint64_t gi) { return gi * 2 + g; };
+    // block index of step gi (past the batch: a repeat of a step of this
+    // wave, cache-hot, as in K1's last prefetch; its result is not stored)
+    auto j_of = [&](uint64_t gi) -> uint64_t {
+        const uint64_t gu = gi < ngroups ? gi : gi - gstep < ngroups ? gi - gstep : ngroups - 1;
+        const uint64_t j = gu * 2 + g;
+        return j < n ? j : n - 1;
+    };
+    // descriptor of block j (planned: of its span sj)
+    auto rec_of = [&](uint64_t j, uint32_t sj) -> uint4 {
+        if (IDENT) {
+            // (offsets or stride is a template choice: a load under a branch
+            // leaves the waitcnt pass a merged state that drains the prefetch)
+            const uint64_t off = OFFS ? a.offsets[j] : j * a.stride;
+            return make_uint4((uint32_t)off, (uint32_t)(off >> 32), a.len, 0u);
+        }
+        return irec[sj];
+    };
+    auto block_of = [&](const uint4 &r) -> const uint8_t * {
+        const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
+        bool sane = !(r.y & kInsane);
+        if (IDENT) sane = off <= a.base_bytes && r.z <= a.base_bytes - off;  // (as decode_unit)
+        const uint8_t *g1;
+        bool none;
+        one_block(a.base + off, r.z, &g1, &none);
+        return sane && !none ? g1 : zero;  // (no unit: R = 0)
+    };
+    // Loads run ahead of their use (vmcnt counts in issue order, so when a
+    // value is needed only newer loads may be pending): the span index four
+    // steps ahead, the descriptor two, the block one.
+    auto ld = [&](BlkRegs &b, uint64_t gi) {
+        if (IDENT && !OFFS) {  // (fixed stride: nothing to load ahead)
+            b.d.load(block_of(rec_of(j_of(gi), 0u)), li);
+        } else {
+            const uint8_t *blk = block_of(b.rec);
+            if (!IDENT) {
+                b.cur = b.rs;
+                b.rs = b.sidx;
+            }
+            b.rec = rec_of(j_of(gi + 2 * gstep), b.rs);
+            if (!IDENT) b.sidx = fastidx[j_of(gi + 4 * gstep)];
+            b.d.load(blk, li);
+        }
+        // (as K1: the loads stay at the top of the step instead of being sunk
+        // into the chains, where the next step would wait on them at once)
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto part0 = [&](const BlkRegs &b) { return reduce_level<0>(lane_partial_x3s<32>(b.d, c), (lane & 1u) == 0u); };
+    uint32_t *dst = IDENT ? a.out : a.span_acc;
+    auto store = [&](uint32_t raw, uint64_t gi, uint32_t span, bool on) {
+        const uint64_t item = item_of(gi);
+        if (on && gi < ngroups && item < n) dst[IDENT ? item : span] = raw;
+    };
+    BlkRegs ra, rb;
+    if (!IDENT || OFFS) {
+        if (!IDENT) {
+            ra.rs = fastidx[j_of(grp)];
+            rb.rs = fastidx[j_of(grp + gstep)];
+            ra.sidx = fastidx[j_of(grp + 2 * gstep)];
+            rb.sidx = fastidx[j_of(grp + 3 * gstep)];
+        }
+        ra.rec = rec_of(j_of(grp), ra.rs);
+        rb.rec = rec_of(j_of(grp + gstep), rb.rs);
+    }
+    const uint64_t nsteps = (ngroups - grp + gstep - 1) / gstep;
+    ld(ra, grp);
+    uint64_t k = 0;
+    for (; k + 4 <= nsteps; k += 4) {
+        ld(rb, grp + gstep);
+        const uint32_t va = part0(ra), sa = ra.cur;
+        ld(ra, grp + 2 * gstep);
+        const uint32_t vb = part0(rb), sb = rb.cur;
+        const uint32_t vab = group_pair_level1(va, vb, lane);
+        ld(rb, grp + 3 * gstep);
+        const uint32_t vc = part0(ra), sc = ra.cur;
+        ld(ra, grp + 4 * gstep);
+        const uint32_t vd = part0(rb), sd = rb.cur;
+        const uint32_t raw = group_reduce32_quad(vab, group_pair_level1(vc, vd, lane), lane);
+        const uint32_t sp = li == 0 ? sa : li == 1 ? sb : li == 2 ? sc : sd;
+        store(raw, grp + (li & 3u) * gstep, sp, li < 4);
+        grp += 4 * gstep;
+    }
+    for (; k + 2 <= nsteps; k += 2) {
+        ld(rb, grp + gstep);
+        const uint32_t va = part0(ra), sa = ra.cur;
+        ld(ra, grp + 2 * gstep);
+        const uint32_t vb = part0(rb), sb = rb.cur;
+        const uint32_t raw = group_reduce32_pair(va, vb, lane);
+        store(raw, li == 0 ? grp : grp + gstep, li == 0 ? sa : sb, li < 2);
+        grp += 2 * gstep;
+    }
+    if (nsteps & 1) store(group_reduce32_dpp(lane_partial_x3s<32>(ra.d, c), lane), grp, ra.cur, li == 0);
 }
 
 // Chained CRC over an iov list (the chunked-item read verify of

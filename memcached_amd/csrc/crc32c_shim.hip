@@ -105,6 +105,8 @@ struct Device {
     uint32_t *segpow = nullptr;  // rows x^i * x^(8*64Ki*k): k < 256, then k = 256 j
     mcrc_dev::UnitRec *units = nullptr, *whole = nullptr;
     uint4 *irec = nullptr;  // per-span record written by k_count
+    uint8_t *fast = nullptr;     // per span: its unit is one whole block (k_blocks takes it)
+    uint32_t *fastidx = nullptr; // the fast spans' indices, compacted (hipcub DeviceSelect)
     uint32_t *big = nullptr;  // spans expanded by k_expand_big
     void *scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
@@ -224,6 +226,9 @@ int init_device(Device &d, int id) {
         (const void *)mcrc_dev::k_small<0>,
         (const void *)mcrc_dev::k_small<1>,
         (const void *)mcrc_dev::k_small<2>,
+        (const void *)mcrc_dev::k_blocks<false, true>,
+        (const void *)mcrc_dev::k_blocks<true, true>,
+        (const void *)mcrc_dev::k_blocks<true, false>,
     };
     for (const void *k : spans)
         HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImageK1Bytes));
@@ -265,15 +270,21 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
         (void)hipFree(d.irec);
         (void)hipFree(d.span_acc);
         (void)hipFree(d.big);
+        (void)hipFree(d.fast);
+        (void)hipFree(d.fastidx);
         d.plan_items = 0;
         if (hipMalloc(&d.nunit, n * 4) != hipSuccess || hipMalloc(&d.prefix, n * 4) != hipSuccess ||
             hipMalloc(&d.whole, n * sizeof(mcrc_dev::UnitRec)) != hipSuccess ||
             hipMalloc(&d.irec, n * sizeof(uint4)) != hipSuccess || hipMalloc(&d.span_acc, n * 4) != hipSuccess ||
-            hipMalloc(&d.big, n * 4) != hipSuccess)
+            hipMalloc(&d.big, n * 4) != hipSuccess || hipMalloc(&d.fast, n) != hipSuccess ||
+            hipMalloc(&d.fastidx, n * 4) != hipSuccess)
             return CRC32C_ENOMEM;
-        size_t need = 0;
-        if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, d.nunit, d.prefix, (int)n) != hipSuccess)
+        size_t need = 0, need2 = 0;
+        if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, d.nunit, d.prefix, (int)n) != hipSuccess ||
+            hipcub::DeviceSelect::Flagged(nullptr, need2, hipcub::CountingInputIterator<uint32_t>(0), d.fast,
+                                          d.fastidx, d.counters, (int)n) != hipSuccess)
             return CRC32C_EHIP;
+        need = std::max(need, need2);
         if (need > d.scan_tmp_bytes) {
             (void)hipFree(d.scan_tmp);
             if (hipMalloc(&d.scan_tmp, need) != hipSuccess) return CRC32C_ENOMEM;
@@ -290,6 +301,17 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
     }
     if (!d.counters && hipMalloc(&d.counters, 16) != hipSuccess) return CRC32C_ENOMEM;
     return CRC32C_OK;
+}
+
+// Every span of `len` bytes is one whole block at its G1 (mcrc_dev::one_block)
+// whatever its alignment (p & 15): the identity batch can go to k_blocks.
+bool one_block_len(uint32_t len) {
+    for (uint32_t kh = 0; kh < 16; ++kh) {
+        const uint32_t vlen = len + ((0u - kh - len) & (mcrc_dev::kTailAlign - 1)), x = vlen + kh;
+        const uint32_t g1o = x - mcrc_dev::kBlockBytes * ((x - 1) / mcrc_dev::kBlockBytes) - kh;
+        if (!(len && g1o <= mcrc_dev::kFragMax && vlen - g1o == mcrc_dev::kBlockBytes)) return false;
+    }
+    return true;
 }
 
 // Batches of at most this many spans take the single-launch k_small.
@@ -332,7 +354,18 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     }
     if (identity) {
         // (spans of at most kFragMax - 127 bytes are all their threads' in k_final)
-        if (a.len + mcrc_dev::kTailAlign - 1 > mcrc_dev::kFragMax) spans(a, grid_for(d, n));
+        if (a.len + mcrc_dev::kTailAlign - 1 > mcrc_dev::kFragMax) {
+            if (one_block_len(a.len) && a.offsets)
+                hipLaunchKernelGGL((mcrc_dev::k_blocks<true, true>), dim3(grid_for(d, n)), dim3(1024),
+                                   mcrc_dev::kLdsImageK1Bytes, st, a, d.img_k1, (const uint4 *)nullptr,
+                                   (const uint32_t *)nullptr, (const uint32_t *)nullptr);
+            else if (one_block_len(a.len))
+                hipLaunchKernelGGL((mcrc_dev::k_blocks<true, false>), dim3(grid_for(d, n)), dim3(1024),
+                                   mcrc_dev::kLdsImageK1Bytes, st, a, d.img_k1, (const uint4 *)nullptr,
+                                   (const uint32_t *)nullptr, (const uint32_t *)nullptr);
+            else
+                spans(a, grid_for(d, n));
+        }
         hipLaunchKernelGGL((mcrc_dev::k_final<0, false>), dim3(gf), dim3(256), 0, st, a, nullptr);
         HIP_OK(hipGetLastError());
         return CRC32C_OK;
@@ -343,13 +376,16 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     const uint64_t cap = std::min<uint64_t>(n + a.base_bytes / mcrc_dev::kSegBytes + 1 + n / 4096, 0xfffffff0ull);
     int rc = ensure_plan(d, n, cap);
     if (rc) return rc;
-    uint32_t *nvalid = d.counters, *nwhole = d.counters + 1, *nbig = d.counters + 2;
+    uint32_t *nvalid = d.counters, *nwhole = d.counters + 1, *nbig = d.counters + 2, *nfast = d.counters + 3;
     HIP_OK(hipMemsetAsync(nvalid, 0xff, 4, st));
     HIP_OK(hipMemsetAsync(nwhole, 0, 8, st));  // nwhole, nbig
     a.span_acc = d.span_acc;
-    hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nunit, d.irec);
+    hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nunit, d.irec, d.fast);
     size_t tmp = d.scan_tmp_bytes;
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(d.scan_tmp, tmp, d.nunit, d.prefix, (int)n, st));
+    tmp = d.scan_tmp_bytes;
+    HIP_OK(hipcub::DeviceSelect::Flagged(d.scan_tmp, tmp, hipcub::CountingInputIterator<uint32_t>(0), d.fast,
+                                         d.fastidx, nfast, (int)n, st));
     hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(g1), dim3(256), 0, st, a.base, d.nunit, d.prefix, d.irec, n, d.units,
                        cap, nvalid, d.whole, nwhole, d.big, nbig);
     hipLaunchKernelGGL(mcrc_dev::k_expand_big, dim3(1024), dim3(256), 0, st, a.base, d.nunit, d.prefix, d.irec,
@@ -359,6 +395,10 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     u.nunits = nvalid;
     u.span_acc = d.span_acc;
     u.segpow = d.segpow;
+    // spans whose unit is one whole block: k_blocks over the compacted list;
+    // the other spans' units: the span kernel
+    hipLaunchKernelGGL((mcrc_dev::k_blocks<false, true>), dim3(grid_for(d, n)), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st,
+                       u, d.img_k1, (const uint4 *)d.irec, (const uint32_t *)d.fastidx, (const uint32_t *)nfast);
     spans(u, d.cus);
     mcrc_dev::SpanArgs w = u;  // (every table pointer set, even those whole units do not use)
     w.units = d.whole;
