@@ -657,8 +657,9 @@ __device__ __forceinline__ SpanHead span_head(const uint8_t *p, uint32_t len) {
     return {g1o, len != 0 && g1o <= kFragMax};
 }
 
-// One-block geometry of span [p, p + len): true (and G1) if its unit is one
-// whole block at G1 = p + g1o, or it has no unit at all (false: neither).
+// One-block geometry of span [p, p + len): true if its unit is one whole block
+// (at G1 when its head fragment is the thread's, else at ph; *g1 = the block),
+// or it has no unit at all (*none); false: neither.
 __device__ __forceinline__ bool one_block(const uint8_t *p, uint32_t len, const uint8_t **g1, bool *none) {
     const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
     const uint32_t vlen = len + tail_pad(p, len);
@@ -666,6 +667,10 @@ __device__ __forceinline__ bool one_block(const uint8_t *p, uint32_t len, const 
     const uint32_t g1o = x - kBlockBytes * ((x - 1) / kBlockBytes) - kh;
     const bool drop = len != 0 && g1o <= kFragMax;
     *none = len == 0 || (drop && g1o == vlen);
+    if (!drop && x == kBlockBytes) {  // the unit [ph, Ea) is itself one block
+        *g1 = p - kh;
+        return true;
+    }
     *g1 = p + g1o;
     return *none || (drop && vlen - g1o == kBlockBytes);
 }

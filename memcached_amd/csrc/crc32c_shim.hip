@@ -309,7 +309,8 @@ bool one_block_len(uint32_t len) {
     for (uint32_t kh = 0; kh < 16; ++kh) {
         const uint32_t vlen = len + ((0u - kh - len) & (mcrc_dev::kTailAlign - 1)), x = vlen + kh;
         const uint32_t g1o = x - mcrc_dev::kBlockBytes * ((x - 1) / mcrc_dev::kBlockBytes) - kh;
-        if (!(len && g1o <= mcrc_dev::kFragMax && vlen - g1o == mcrc_dev::kBlockBytes)) return false;
+        const bool drop = len && g1o <= mcrc_dev::kFragMax;
+        if (!(drop ? vlen - g1o == mcrc_dev::kBlockBytes : len && x == mcrc_dev::kBlockBytes)) return false;
     }
     return true;
 }

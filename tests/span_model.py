@@ -129,3 +129,16 @@ def xpow8_inv(t):
         assert target == 0
         _INV[t] = comb
     return _INV[t]
+
+
+def one_block(p, length):
+    """(is one block or none, none, G1) -- k_blocks' test (crc32c_kernels.hip one_block)."""
+    kh = p & 15
+    vlen = length + tail_pad(p, length)
+    x = vlen + kh
+    g1o = x - BLOCK * ((x - 1) // BLOCK) - kh if length else 0
+    drop = length != 0 and g1o <= FRAG_MAX
+    none = length == 0 or (drop and g1o == vlen)
+    if not drop and x == BLOCK:  # the unit [ph, Ea) is itself one block
+        return True, False, p - kh
+    return none or (drop and vlen - g1o == BLOCK), none, p + g1o

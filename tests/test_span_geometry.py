@@ -68,3 +68,20 @@ def test_head_fragment_rule():
         p, length = 5, 3 * SEG + extra
         vlen = length + tail_pad(p, length)
         assert len(units_of(0, p, length)) == nseg_of(vlen) - lost
+
+
+def test_one_block_matches_the_unit_plan():
+    """k_blocks takes a span iff the planner would give it exactly one unit of
+    one whole block (and the same block), and no unit at all iff it has none."""
+    from tests.span_model import one_block
+    rng = np.random.default_rng(5)
+    for _ in range(3000):
+        p = int(rng.integers(0, 1 << 20))
+        length = int(rng.choice([rng.integers(0, 9000), rng.integers(4000, 5200)]))
+        fast, none, g1 = one_block(p, length)
+        units = units_of(0, p, length)
+        assert none == (len(units) == 0)
+        one = len(units) == 1 and units[0][2] == 1 and (units[0][1] + (units[0][0] & 15)) == BLOCK
+        assert (fast and not none) == one, (p, length)
+        if one:  # the block k_blocks reads is the unit's block
+            assert units[0][0] - (units[0][0] & 15) == g1
