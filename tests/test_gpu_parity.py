@@ -591,6 +591,34 @@ def _mixed_page(rng, n_items, wbuf, max_value):
     return buf, offs
 
 
+def test_verify_4165_items_with_corrupt_lengths(torch):
+    """The config-5 shape: packed 4165-B images (one 4 KiB block each after
+    the head fragment, k_blocks), a few with a flipped bit in nbytes (their
+    spans leave the one-block shape, or the wbuf: the span kernel, or not
+    sane) and a few with a flipped data bit.  Exactly the corrupted images
+    fail, through both kernels in one call; a stamp then repairs the data
+    flips in place."""
+    rng = np.random.default_rng(4165)
+    n = 3000
+    items = [layout.make_item(b"key%07d" % i, rng.integers(0, 256, 4096, dtype=np.uint8).tobytes(), cas=i + 1)
+             for i in range(n)]
+    assert len(items[0]) == 4165
+    buf, offs = layout.pack_wbufs(items, 1 << 20)
+    soffs, slens = layout.spans_of(buf, offs)
+    layout.store_crcs(buf, offs, oracle.batch(buf, soffs, slens))
+    victims = rng.choice(n, 60, replace=False)
+    hdr, data = victims[:30], victims[30:]
+    for v in hdr:  # nbytes (bytes 32..35): a length bit
+        buf[int(offs[v]) + 32 + int(rng.integers(0, 2))] ^= 1 << int(rng.integers(0, 8))
+    for v in data:
+        buf[int(soffs[v] + rng.integers(16, slens[v]))] ^= 1 << int(rng.integers(0, 8))
+    ok, nbad = mc.verify_items(_dev(torch, buf), _dev(torch, offs.view(np.int64)), region_bytes=1 << 20)
+    want = np.ones(n, np.uint8)
+    want[victims] = 0
+    assert nbad == victims.size
+    np.testing.assert_array_equal(ok.cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("max_value", [24, 700, 9000])
 def test_page_stream_tiny_to_large_items(torch, max_value):
     """Item images from ~52 B (more than 32 spans per 4 KiB block) to ~9 KB,
