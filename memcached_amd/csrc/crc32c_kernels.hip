@@ -473,7 +473,10 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 constexpr uint32_t kSpanCH = 32;
 constexpr uint32_t kRowBytes = 32 * kSpanCH;  // 1024
 constexpr uint32_t kBlockBytes = 4 * kRowBytes;  // 4096
-constexpr uint32_t kSegBytes = 64 * 1024;
+#ifndef MCRC_SEG_KIB
+#define MCRC_SEG_KIB 64
+#endif
+constexpr uint32_t kSegBytes = MCRC_SEG_KIB * 1024;
 constexpr uint32_t kWhole = 0xffffffffu;      // unit segment index: the whole span
 // Pieces outside a span are read from a zeroed buffer; workgroup b reads the
 // 16 B at zero + 4 KiB * (b % 256), so the workgroups' zero reads spread over

@@ -190,14 +190,14 @@ int init_device(Device &d, int id) {
     mcrc::build_lds_image_k1(img_k1.data(), kFixedCH);
     HIP_OK(hipMalloc(&d.img_k1, img_k1.size() * 4));
     HIP_OK(hipMemcpy(d.img_k1, img_k1.data(), img_k1.size() * 4, hipMemcpyHostToDevice));
-    std::vector<uint32_t> sp(512 * 32);
-    for (uint32_t k = 0; k < 256; ++k) {
-        const uint32_t lo = mcrc::xpow8n((uint64_t)mcrc_dev::kSegBytes * k);
-        const uint32_t hi = mcrc::xpow8n((uint64_t)mcrc_dev::kSegBytes * 256 * k);
-        for (uint32_t i = 0; i < 32; ++i) {
-            sp[k * 32 + i] = mcrc::mulmodp(0x80000000u >> i, lo);
-            sp[(256 + k) * 32 + i] = mcrc::mulmodp(0x80000000u >> i, hi);
-        }
+    // rows k (k < 256) and 256 + j (x^(8 * kSegBytes * 256 j)) for every
+    // segment count of a 4 GiB span
+    const uint32_t nhi = (uint32_t)((((1ull << 32) + 16) / mcrc_dev::kSegBytes + 1 + 255) / 256);
+    std::vector<uint32_t> sp((256 + std::max(nhi, 256u)) * 32);
+    for (uint32_t k = 0; k < 256 + std::max(nhi, 256u); ++k) {
+        const uint64_t segs = k < 256 ? k : 256ull * (k - 256);
+        const uint32_t y = mcrc::xpow8n((uint64_t)mcrc_dev::kSegBytes * segs);
+        for (uint32_t i = 0; i < 32; ++i) sp[k * 32 + i] = mcrc::mulmodp(0x80000000u >> i, y);
     }
     HIP_OK(hipMalloc(&d.segpow, sp.size() * 4));
     HIP_OK(hipMemcpy(d.segpow, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
