@@ -1399,13 +1399,16 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
     auto item_of = [&](uint64_t gi) { return gi * 2 + g; };
     // block index of step gi (past the batch: a repeat of a step of this
     // wave, cache-hot, as in K1's last prefetch; its result is not stored)
-    auto j_of = [&](uint64_t gi) -> uint64_t {
-        const uint64_t gu = gi < ngroups ? gi : gi - gstep < ngroups ? gi - gstep : ngroups - 1;
-        const uint64_t j = gu * 2 + g;
-        return j < n ? j : n - 1;
+    // (32-bit: the shim keeps n below 2^32)
+    const uint32_t n32 = (uint32_t)n, ng32 = (uint32_t)ngroups, gstep32 = (uint32_t)gstep;
+    auto j_of = [&](uint64_t gi64) -> uint32_t {
+        const uint32_t gi = (uint32_t)gi64;
+        const uint32_t gu = gi < ng32 ? gi : gi - gstep32 < ng32 ? gi - gstep32 : ng32 - 1;
+        const uint32_t j = gu * 2 + g;
+        return j < n32 ? j : n32 - 1;
     };
     // descriptor of block j (planned: of its span sj)
-    auto rec_of = [&](uint64_t j, uint32_t sj) -> uint4 {
+    auto rec_of = [&](uint32_t j, uint32_t sj) -> uint4 {
         if (IDENT) {
             // (offsets or stride is a template choice: a load under a branch
             // leaves the waitcnt pass a merged state that drains the prefetch)
@@ -1414,14 +1417,15 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
         }
         return irec[sj];
     };
+    // A span here is one whole block and has a unit (one_block), so its block
+    // is [Ea - 4096, Ea) whichever case of one_block holds.
     auto block_of = [&](const uint4 &r) -> const uint8_t * {
         const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
         bool sane = !(r.y & kInsane);
         if (IDENT) sane = off <= a.base_bytes && r.z <= a.base_bytes - off;  // (as decode_unit)
-        const uint8_t *g1;
-        bool none;
-        one_block(a.base + off, r.z, &g1, &none);
-        return sane && !none ? g1 : zero;  // (no unit: R = 0)
+        const uint8_t *e = a.base + off + r.z;
+        const uint8_t *blk = e + ((0u - (uint32_t)(uintptr_t)e) & 15u) - kBlockBytes;  // (pointer
+        return sane ? blk : zero;  // arithmetic: an integer round trip would make these flat loads)
     };
     // Loads run ahead of their use (vmcnt counts in issue order, so when a
     // value is needed only newer loads may be pending): the span index four
