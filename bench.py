@@ -307,6 +307,75 @@ def workload_config5(args, rank, world):
             "injected_bad": int(victims.numel())}
 
 
+def workload_pagesmix(args, rank, world):
+    """Extstore pages of packed item images of mixed sizes, stored CRCs verified.
+
+    Not a BASELINE config: a realistic page mix next to config 5's equal
+    4165-B items.  Values are log-uniform 512 B - 64 KiB (extstore keeps items
+    below ext_item_size = 512 B in RAM), key%07d keys, CAS; each 4 MiB wbuf is
+    packed until the next item would not fit (extstore.c:591-670) and the rest
+    zeroed; 1 % of items get one flipped bit."""
+    import numpy as np
+    wbuf, nwb = 4 << 20, args.pages * 16
+    rng = np.random.default_rng(17 + rank)
+    vals = np.exp(rng.uniform(np.log(512), np.log(65536), (nwb, 1024))).astype(np.int64)
+    ntot = vals + 2 + 48 + 10 + 1 + 8                    # value + CRLF, header, key + NUL, CAS
+    ends = np.cumsum(ntot, axis=1)
+    keep = ends <= wbuf
+    starts = ends - ntot
+    offs_np = (np.arange(nwb, dtype=np.int64)[:, None] * wbuf + starts)[keep]
+    ntot_np, vals_np = ntot[keep], vals[keep]
+    n = int(offs_np.size)
+    g = torch.Generator(device="cuda").manual_seed(9 + rank)
+    data = torch.randint(0, 256, (nwb * wbuf,), dtype=torch.uint8, device="cuda", generator=g)
+    wb = data.view(nwb, wbuf)
+    for w, t in enumerate(np.where(keep, ends, 0).max(axis=1).tolist()):  # zero each wbuf's tail
+        wb[w, t:] = 0
+    offs = torch.from_numpy(offs_np).cuda()
+    idx = torch.arange(n, device="cuda", dtype=torch.int64)
+    nbytes = torch.from_numpy(vals_np + 2).cuda()
+    le = lambda v, k: torch.stack([(v >> (8 * i)) & 0xFF for i in range(k)], -1).to(torch.uint8)
+    hdr = torch.zeros(n, 67, dtype=torch.uint8, device="cuda")
+    hdr[:, 24:28] = le(idx * 2654435761 & 0xFFFFFFFF, 4)          # time (hash)
+    hdr[:, 32:36] = le(nbytes, 4)                                  # nbytes (value + CRLF)
+    hdr[:, 36] = 1                                                 # refcount
+    hdr[:, 38] = 2                                                 # it_flags = ITEM_CAS
+    hdr[:, 40] = 17                                                # slabs_clsid
+    hdr[:, 41] = 10                                                # nkey
+    hdr[:, 48:56] = le(idx + 1, 8)                                 # CAS
+    hdr[:, 56:59] = torch.tensor(list(b"key"), dtype=torch.uint8, device="cuda")
+    for d in range(7):                                             # key%07d
+        hdr[:, 65 - d] = (48 + (idx // 10 ** d) % 10).to(torch.uint8)
+    flat = data.view(-1)
+    flat[(offs[:, None] + torch.arange(67, device="cuda")[None, :]).reshape(-1)] = hdr.reshape(-1)
+    end = offs + torch.from_numpy(ntot_np).cuda()
+    flat[end - 2] = 13
+    flat[end - 1] = 10
+    # spill CRCs (storage.c:567) into exptime, computed by the span kernel
+    span_offs = (offs + 32).contiguous()
+    span_lens = torch.from_numpy((ntot_np - 32).astype(np.int32)).cuda()
+    crc = torch.empty(n, dtype=torch.int32, device="cuda")
+    sp = _lib.Spans(data.data_ptr(), data.numel(), span_offs.data_ptr(), 0, span_lens.data_ptr(), 0, None,
+                    crc.data_ptr(), n)
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp), _lib.CRC32C_DEVICE, None))
+    flat[(offs[:, None] + 28 + torch.arange(4, device="cuda")[None, :]).reshape(-1)] = crc.view(torch.uint8)
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    victims = torch.randperm(n, device="cuda", generator=gen)[: n // 100]
+    span = span_lens[victims].to(torch.int64)
+    pos = offs[victims] + 32 + (torch.rand(victims.numel(), device="cuda", generator=gen) * span).to(torch.int64)
+    bit = torch.randint(0, 8, (victims.numel(),), device="cuda", generator=gen).to(torch.uint8)
+    flat[pos] ^= (torch.ones_like(bit) << bit)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    _KEEP.extend((data, offs))
+    span_bytes = int((ntot_np - 32).sum())
+    return (data.data_ptr(), data.numel(), wbuf, offs.data_ptr(), n, ok.data_ptr()), ok, victims, span_bytes, {
+        "workload": f"{args.pages} x 64 MiB extstore pages of mixed items (values log-uniform 512 B - 64 KiB, "
+                    f"mean item {int(ntot_np.mean())} B), packed per 4 MiB wbuf, stored CRC verified per item",
+        "pages_per_gpu": args.pages, "items_per_gpu": n, "span_bytes_per_gpu": span_bytes,
+        "items_le_4k_frac": round(float((ntot_np <= 4096).mean()), 3), "injected_bad": int(victims.numel())}
+
+
 def traffic_per_launch():
     """HBM bytes per K1 launch from the committed rocprofv3 --pmc summary, if any."""
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
@@ -338,7 +407,7 @@ def main():
     ap.add_argument("--fill", default="splitmix", choices=["splitmix", "randint"],
                     help="item bytes: splitmix64(42 + rank) words (SURVEY.md 8d) or torch.randint")
     ap.add_argument("--workload", default="config2",
-                    choices=["config2", "config2r", "config3", "config5", "pages", "stamp", "host", "calls"],
+                    choices=["config2", "config2r", "config3", "config5", "pagesmix", "pages", "stamp", "host", "calls"],
                     help="config2 = headline; others are extra measurements (not the bench line)")
     ap.add_argument("--pages", type=int, default=1000, help="config5: 64 MiB pages per GPU")
     ap.add_argument("--span-len", type=int, default=4133, help="config2r: span length (stride = len + 32)")
@@ -425,8 +494,9 @@ def extra_workload(args):
         kms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
         res.update(config=cfg, kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
                    hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
-    elif args.workload == "config5":
-        vargs, ok, victims, nbytes, cfg = workload_config5(args, rank, world)
+    elif args.workload in ("config5", "pagesmix"):
+        vargs, ok, victims, nbytes, cfg = (workload_config5 if args.workload == "config5" else
+                                           workload_pagesmix)(args, rank, world)
         run_verify_steps(vargs, max(1, args.warmup), stream)
         torch.cuda.synchronize()
         elapsed, (evs, nbad) = timed(lambda k: run_verify_steps(vargs, k, stream), args.steps, world)

@@ -646,9 +646,19 @@ __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, ui
 // bytes instead (reg_advance), the head unit starts at G1, and a span that
 // fits one block is not given to the span kernel at all.
 #ifndef MCRC_FRAG_MAX
-#define MCRC_FRAG_MAX 1024
+#define MCRC_FRAG_MAX 128
 #endif
-constexpr uint32_t kFragMax = MCRC_FRAG_MAX;
+#ifndef MCRC_WHOLE_MAX
+#define MCRC_WHOLE_MAX 1024
+#endif
+constexpr uint32_t kFragMax = MCRC_FRAG_MAX;    // a head fragment [p, G1) of at most this
+constexpr uint32_t kWholeMax = MCRC_WHOLE_MAX;  // a whole span of vlen at most this
+static_assert(kWholeMax + 16 <= kBlockBytes, "a whole span held by its thread is its own fragment (G1 = Ea)");
+// Is the head fragment (G1 - p = g1o) the span thread's?  For vlen <= kWholeMax
+// the fragment is the whole span (G1 = Ea).
+__device__ __forceinline__ bool frag_drop(uint32_t len, uint64_t g1o, uint64_t vlen) {
+    return len != 0 && (g1o <= kFragMax || vlen <= kWholeMax);
+}
 struct SpanHead {
     uint64_t g1o;  // G1 - p
     bool drop;     // [p, G1) is the thread's
@@ -657,18 +667,18 @@ __device__ __forceinline__ SpanHead span_head(const uint8_t *p, uint32_t len) {
     const uint64_t kh = (uintptr_t)p & 15u;
     const uint64_t x = (uint64_t)len + tail_pad(p, len) + kh;  // Ea - ph
     const uint64_t g1o = x - kBlockBytes * ((x - 1) / kBlockBytes) - kh;
-    return {g1o, len != 0 && g1o <= kFragMax};
+    return {g1o, frag_drop(len, g1o, x - kh)};
 }
 
 // One-block geometry of span [p, p + len): true if its unit is one whole block
 // (at G1 when its head fragment is the thread's, else at ph; *g1 = the block),
 // or it has no unit at all (*none); false: neither.
 __device__ __forceinline__ bool one_block(const uint8_t *p, uint32_t len, const uint8_t **g1, bool *none) {
-    const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
-    const uint32_t vlen = len + tail_pad(p, len);
-    const uint32_t x = vlen + kh;  // Ea - ph
-    const uint32_t g1o = x - kBlockBytes * ((x - 1) / kBlockBytes) - kh;
-    const bool drop = len != 0 && g1o <= kFragMax;
+    const uint64_t kh = (uintptr_t)p & 15u;
+    const uint64_t vlen = (uint64_t)len + tail_pad(p, len);  // (64-bit: len may be close to 2^32)
+    const uint64_t x = vlen + kh;  // Ea - ph
+    const uint64_t g1o = x - kBlockBytes * ((x - 1) / kBlockBytes) - kh;
+    const bool drop = frag_drop(len, g1o, vlen);
     *none = len == 0 || (drop && g1o == vlen);
     if (!drop && x == kBlockBytes) {  // the unit [ph, Ea) is itself one block
         *g1 = p - kh;
@@ -844,7 +854,7 @@ __device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw,
         const uint32_t vlen = len + ((0u - plo - len) & (kTailAlign - 1));  // tail_pad
         const uint32_t x = vlen + kh;  // Ea - ph
         const uint32_t g1o = x - kBlockBytes * ((x - 1) >> 12) - kh;  // span_head
-        const uint32_t po = len && g1o <= kFragMax ? g1o : 0u;
+        const uint32_t po = frag_drop(len, g1o, vlen) ? g1o : 0u;
         const uint32_t eo = vlen - po;
         const uint32_t niters = len ? (eo + ((kh + po) & 15u) + kBlockBytes - 1) >> 12 : 0u;
         d.p = a.base + (sane ? off : 0) + po;

@@ -309,7 +309,7 @@ bool one_block_len(uint32_t len) {
     for (uint32_t kh = 0; kh < 16; ++kh) {
         const uint32_t vlen = len + ((0u - kh - len) & (mcrc_dev::kTailAlign - 1)), x = vlen + kh;
         const uint32_t g1o = x - mcrc_dev::kBlockBytes * ((x - 1) / mcrc_dev::kBlockBytes) - kh;
-        const bool drop = len && g1o <= mcrc_dev::kFragMax;
+        const bool drop = len && (g1o <= mcrc_dev::kFragMax || vlen <= mcrc_dev::kWholeMax);  // frag_drop
         if (!(drop ? vlen - g1o == mcrc_dev::kBlockBytes : len && x == mcrc_dev::kBlockBytes)) return false;
     }
     return true;
@@ -354,8 +354,8 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
         return CRC32C_OK;
     }
     if (identity) {
-        // (spans of at most kFragMax - 127 bytes are all their threads' in k_final)
-        if (a.len + mcrc_dev::kTailAlign - 1 > mcrc_dev::kFragMax) {
+        // (spans of at most kWholeMax - 15 bytes are all their threads' in k_final)
+        if (a.len + mcrc_dev::kTailAlign - 1 > mcrc_dev::kWholeMax) {
             if (one_block_len(a.len) && a.offsets)
                 hipLaunchKernelGGL((mcrc_dev::k_blocks<true, true>), dim3(grid_for(d, n)), dim3(1024),
                                    mcrc_dev::kLdsImageK1Bytes, st, a, d.img_k1, (const uint4 *)nullptr,

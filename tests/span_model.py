@@ -6,7 +6,8 @@ without a GPU."""
 SEG = 64 * 1024
 BLOCK = 4096
 WHOLE = 0xFFFFFFFF
-FRAG_MAX = 1024
+FRAG_MAX = 128    # kFragMax: a head fragment [p, G1) of at most this is the thread's
+WHOLE_MAX = 1024  # kWholeMax: so is a whole span of vlen at most this
 POLY = 0x82F63B78
 M32 = 0xFFFFFFFF
 
@@ -26,7 +27,11 @@ def span_head(p, length):
     kh = p & 15
     x = length + tail_pad(p, length) + kh
     g1o = x - BLOCK * ((x - 1) // BLOCK) - kh if length else 0
-    return g1o, length != 0 and g1o <= FRAG_MAX
+    return g1o, frag_drop(length, g1o, length + tail_pad(p, length))
+
+
+def frag_drop(length, g1o, vlen):
+    return length != 0 and (g1o <= FRAG_MAX or vlen <= WHOLE_MAX)
 
 
 def span_units(p, length):
@@ -137,7 +142,7 @@ def one_block(p, length):
     vlen = length + tail_pad(p, length)
     x = vlen + kh
     g1o = x - BLOCK * ((x - 1) // BLOCK) - kh if length else 0
-    drop = length != 0 and g1o <= FRAG_MAX
+    drop = frag_drop(length, g1o, vlen)
     none = length == 0 or (drop and g1o == vlen)
     if not drop and x == BLOCK:  # the unit [ph, Ea) is itself one block
         return True, False, p - kh

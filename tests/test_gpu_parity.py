@@ -500,12 +500,13 @@ def test_offsets_with_fixed_length(torch):
     np.testing.assert_array_equal(outh, oracle.batch(host, offs, np.full(n, L)))
 
 
-@pytest.mark.parametrize("L", [1, 15, 100, 896, 897, 898, 1008, 1009, 1010, 1024, 1040, 4080, 4097, 5104, 5125, 8195,
-                               65536, 65552])
+@pytest.mark.parametrize("L", [1, 15, 100, 896, 897, 898, 1008, 1009, 1010, 1024, 1040, 4080, 4097, 4200, 4209, 4224,
+                               4225, 4240, 5104, 5125, 8195, 65536, 65552])
 def test_fixed_length_head_fragment_thresholds(torch, L):
     """offsets[] with one shared length (one unit per span, no plan) at the
     lengths where the head fragment moves between the span kernel and the
-    span's thread (kFragMax = 1024) or the span skips the kernel entirely."""
+    span's thread (kFragMax = 128; whole spans up to kWholeMax = 1024) or the
+    span skips the kernel entirely."""
     import ctypes
     rng = np.random.default_rng(L)
     n = 700

@@ -13,6 +13,15 @@ from tests import oracle
 from tests.span_model import (M32, SEG, mulmodp, span_head, tail_pad, units_of, xpow8, xpow8_inv)
 
 
+@pytest.fixture(autouse=True, params=[(1024, 1024), (256, 1024), (128, 2048)], ids=lambda v: f"frag{v[0]}-whole{v[1]}")
+def limits(request, monkeypatch):
+    """The head-fragment and whole-span limits (kFragMax, kWholeMax) are build
+    constants; the geometry and algebra must hold for any of them."""
+    from tests import span_model
+    monkeypatch.setattr(span_model, "FRAG_MAX", request.param[0])
+    monkeypatch.setattr(span_model, "WHOLE_MAX", request.param[1])
+
+
 def reg(r, data):
     """CRC register advanced from r over data (crc32c(c, D) = ~reg(~c, D))."""
     return ~oracle.crc32c(~r & M32, bytes(data)) & M32

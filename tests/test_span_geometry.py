@@ -12,6 +12,15 @@ import pytest
 from tests.span_model import BLOCK, SEG, WHOLE, make_unit, nseg_of, real_pieces, span_head, tail_pad, units_of
 
 
+@pytest.fixture(autouse=True, params=[(1024, 1024), (256, 1024), (128, 2048)], ids=lambda v: f"frag{v[0]}-whole{v[1]}")
+def limits(request, monkeypatch):
+    """The head-fragment and whole-span limits (kFragMax, kWholeMax) are build
+    constants; the geometry and algebra must hold for any of them."""
+    from tests import span_model
+    monkeypatch.setattr(span_model, "FRAG_MAX", request.param[0])
+    monkeypatch.setattr(span_model, "WHOLE_MAX", request.param[1])
+
+
 def check_units(base, off, length, units):
     P, E = base + off, base + off + length
     covered = np.zeros(length, np.int32)
