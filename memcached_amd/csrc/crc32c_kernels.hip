@@ -619,6 +619,10 @@ __device__ __forceinline__ Piece clear_below(Piece v, uint32_t k) {
 // (leading zeros leave a zero register unchanged), so
 //   r' = M_m(r) ^ raw16(the m bytes at the top).
 // Every load is an aligned piece holding a byte of [p, p + n).
+#ifndef MCRC_ADV_UNROLL
+#define MCRC_ADV_UNROLL 4
+#endif
+constexpr int kAdvUnroll = MCRC_ADV_UNROLL;
 __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, uint32_t n, const Tab8 &t) {
     if (n == 0) return r;
     const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
@@ -632,7 +636,7 @@ __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, ui
         n -= 16u - kh;
         q += 16;
     }
-#pragma unroll 4
+#pragma unroll kAdvUnroll
     for (; n >= 16; n -= 16, q += 16) r = t.piece(r, ld_piece(q));
     if (n) r = t.zeros(r, n) ^ raw16(shl_bytes(ld_piece(q), 16u - n), t);  // bytes [0, n) of the last piece
     return r;
