@@ -588,7 +588,11 @@ struct Tab8 {
                (T(7, d2 & 255u) ^ T(6, (d2 >> 8) & 255u) ^ T(5, (d2 >> 16) & 255u) ^ T(4, d2 >> 24)) ^
                (T(3, d3 & 255u) ^ T(2, (d3 >> 8) & 255u) ^ T(1, (d3 >> 16) & 255u) ^ T(0, d3 >> 24));
     }
-    // M_n(r): the register r advanced over n zero bytes, 1 <= n <= 16
+    // M_4096(r): operator tables 16..19 (slice k: M_4096 of byte b at bits 8k)
+    __device__ __forceinline__ uint32_t block(uint32_t r) const {
+        return (T(16, r & 255u) ^ T(17, (r >> 8) & 255u)) ^ (T(18, (r >> 16) & 255u) ^ T(19, r >> 24));
+    }
+    // M_n(r): the register r advanced over n zero bytes, 0 <= n <= 16
     __device__ __forceinline__ uint32_t zeros(uint32_t r, uint32_t n) const {
         if (n >= 4)
             return T(n - 1, r & 255u) ^ T(n - 2, (r >> 8) & 255u) ^ T(n - 3, (r >> 16) & 255u) ^ T(n - 4, r >> 24);
@@ -597,7 +601,7 @@ struct Tab8 {
         return z;
     }
 };
-constexpr uint32_t kTab8Dwords = 16 * 256;  // 16 KiB
+constexpr uint32_t kTab8Dwords = 20 * 256;  // 16 byte tables + the M_4096 operator, 20 KiB
 // (every thread of the block calls it)
 __device__ __forceinline__ Tab8 load_tab8(uint32_t *s, const uint32_t *tab8) {
     for (uint32_t i = threadIdx.x; i < kTab8Dwords; i += blockDim.x) s[i] = tab8[i];
@@ -705,13 +709,15 @@ __device__ __forceinline__ bool one_block(const uint8_t *p, uint32_t len, const 
 __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
                                               const uint32_t *xp) {
     const uint32_t t = tail_pad(p, len);
-    if (len == 0) return mulmodp_dev(~c, xp[t]);
+    if (len == 0) return t8.zeros(~c, t);
     const uint64_t vlen = (uint64_t)len + t;
     const SpanHead h = span_head(p, len);
-    if (h.drop && h.g1o == vlen) return mulmodp_dev(reg_advance(~c, p, len, t8), xp[t]);
+    if (h.drop && h.g1o == vlen) return t8.zeros(reg_advance(~c, p, len, t8), t);
     uint32_t z;
     if (h.drop) {
-        z = mulmodp_dev(reg_advance(~c, p, (uint32_t)h.g1o, t8), xpow8_dev(xp, vlen - h.g1o));
+        // Ea - G1 is whole blocks; one block (every one-block span) is a table step
+        const uint32_t r = reg_advance(~c, p, (uint32_t)h.g1o, t8);
+        z = vlen - h.g1o == kBlockBytes ? t8.block(r) : mulmodp_dev(r, xpow8_dev(xp, vlen - h.g1o));
     } else {
         const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
         uint32_t y = ~c;
@@ -1156,7 +1162,7 @@ __global__ void k_count(SpanArgs a, uint32_t *nunit, uint4 *irec, uint8_t *fast)
         uint32_t z = 0;
         if (it.sane) {
             z = span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow);
-            if (MODE == 1) z ^= mulmodp_dev(~it.aux, a.xpow[tail_pad(it.p, it.len)]);  // W
+            if (MODE == 1) z ^= t8.zeros(~it.aux, tail_pad(it.p, it.len));  // W
         }
         irec[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32) | (it.sane ? 0u : kInsane), it.len, z);
         a.span_acc[i] = 0u;

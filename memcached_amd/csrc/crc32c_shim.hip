@@ -170,10 +170,13 @@ int init_device(Device &d, int id) {
     mcrc::build_lds_image_span(img.data(), mcrc_dev::kSpanCH);
     std::vector<uint32_t> tab8(mcrc_dev::kTab8Dwords);  // [k][b]: the byte-wise table followed by k zero bytes
     mcrc::build_t0(tab8.data());
-    for (uint32_t k = 1; k < mcrc_dev::kTab8Dwords / 256; ++k) {
+    for (uint32_t k = 1; k < 16; ++k) {
         const mcrc::Gf2Op zk = mcrc::Gf2Op::zeros(k);
         for (uint32_t b = 0; b < 256; ++b) tab8[256 * k + b] = zk.apply(tab8[b]);
     }
+    const mcrc::Gf2Op z4k = mcrc::Gf2Op::zeros(mcrc_dev::kBlockBytes);  // tables 16..19: M_4096 by byte slice
+    for (uint32_t k = 0; k < 4; ++k)
+        for (uint32_t b = 0; b < 256; ++b) tab8[256 * (16 + k) + b] = z4k.apply(b << (8 * k));
     std::vector<uint32_t> xp(mcrc_dev::kXpowDwords);
     for (uint32_t j = 0; j < 1024; ++j) {
         xp[j] = mcrc::xpow8n(j);
