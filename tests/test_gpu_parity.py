@@ -177,6 +177,24 @@ def test_long_spans_cross_segments(torch, aligned):
     np.testing.assert_array_equal(_u32(out), want)
 
 
+def test_very_long_spans(torch):
+    """Spans of more than 256 segments (16 MiB): the segment shift takes the
+    second factor of the shift table (x^(8 * 64Ki * 256 j)); k_expand_big
+    places their units.  Up to 300 MiB, unaligned, with nested spans."""
+    rng = np.random.default_rng(35)
+    size = (300 << 20) + 4096
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    offs = np.array([3, 5, (1 << 20) + 1, 7 << 20, 123, 40 << 20, 9], dtype=np.uint64)
+    lens = np.array([(17 << 20) + 5, (33 << 20) + 1, (16 << 20) + 16, (64 << 20) + 3, 4133, (256 << 20) - 77,
+                     (300 << 20) + 11], dtype=np.uint32)
+    cin = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(host, offs, lens, cin)
+    out = mc.batch(_dev(torch, host), offsets=_dev(torch, offs.view(np.int64)),
+                   lens=_dev(torch, lens.view(np.int32)), crc_in=_dev(torch, cin.view(np.int32)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), want)
+
+
 def test_overlapping_long_spans_whole_pass(torch):
     """Overlapping spans whose units exceed the planner's capacity are processed
     whole by the second pass; results stay exact."""
