@@ -651,8 +651,11 @@ __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, ui
 // same grid); G1 = the first grid point after ph.  The span kernel would
 // spend a whole block step of its group on [p, G1), mostly on rows without a
 // byte of the span; when G1 - p <= kFragMax the span's thread takes those
-// bytes instead (reg_advance), the head unit starts at G1, and a span that
-// fits one block is not given to the span kernel at all.
+// bytes instead (reg_advance), the head unit starts at G1, and a span whose
+// virtual length is at most kWholeMax is not given to the span kernel at all.
+// (The limits are measured: a thread's chain is serial, one LDS round trip
+// per 16 B, so long fragments cost more than the block step they save --
+// DESIGN.md section 3.)
 #ifndef MCRC_FRAG_MAX
 #define MCRC_FRAG_MAX 128
 #endif
