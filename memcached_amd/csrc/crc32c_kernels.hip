@@ -733,46 +733,64 @@ __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, ui
 
 
 
+// Item header fields (memcached.h:613-636) from bytes 28..43 of the image at
+// it, read as the two aligned pieces holding them (every byte of those pieces
+// shares its 16-B granule with a header byte, so no read leaves the image's
+// pages).  ITEM_ntotal as memcached.h:149-152.
+struct ItemHdr {
+    uint32_t exptime;  // bytes 28..31: the spill CRC (storage.c:567)
+    uint32_t nbytes;   // 32..35
+    uint32_t flags;    // it_flags, 38..39
+    uint32_t nkey;     // 41
+    __device__ __forceinline__ uint64_t ntotal() const {
+        return 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) + ((flags & 2u) ? 8 : 0);
+    }
+};
+__device__ __forceinline__ ItemHdr parse_hdr(const uint8_t *it) {
+    const uintptr_t x = (uintptr_t)(it + 28), q = x & ~(uintptr_t)15, q2 = (x + 13) & ~(uintptr_t)15;
+    const Piece v0 = ld_piece((const uint8_t *)q), v1 = ld_piece((const uint8_t *)q2);
+    const uint32_t sh = (uint32_t)(x - q);  // 0..15
+    const uint64_t w0 = v0.lo, w1 = v0.hi, w2 = q2 != q ? v1.lo : 0, w3 = q2 != q ? v1.hi : 0;
+    const uint64_t a0 = sh < 8 ? w0 : w1, a1 = sh < 8 ? w1 : w2, a2 = sh < 8 ? w2 : w3;
+    const uint32_t k = 8 * (sh & 7u);
+    const uint64_t f0 = k ? (a0 >> k) | (a1 << (64 - k)) : a0;  // image bytes 28..35
+    const uint64_t f1 = k ? (a1 >> k) | (a2 << (64 - k)) : a1;  // 36..43
+    return {(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)(f1 >> 16) & 0xffffu, (uint32_t)(f1 >> 40) & 0xffu};
+}
+
+// The CRC span of the item image at base + off with header h (parsed when
+// hdr_ok): [off + 32, off + ITEM_ntotal) (STORE_OFFSET, storage.h:43), the
+// stored CRC in aux.
+__device__ __forceinline__ ItemDesc item_desc(const SpanArgs &a, uint64_t off, const ItemHdr &h, bool hdr_ok) {
+    ItemDesc d;
+    const uint64_t ntotal = h.ntotal();
+    d.aux = h.exptime;
+    // an item never crosses its write buffer (extstore.c:627-636), so a
+    // header claiming otherwise is corrupt
+    const bool in_region = a.region == 0 || off / a.region == (off + ntotal - 1) / a.region;
+    d.sane = hdr_ok && h.nkey != 0 && h.nbytes < 0x80000000u && off + ntotal <= a.base_bytes && in_region;
+    d.p = a.base + off + 32;
+    d.len = d.sane ? (uint32_t)(ntotal - 32) : 0u;
+    return d;
+}
+
 template <int MODE>
 __device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
-    ItemDesc d;
     const uint64_t off = a.offsets ? a.offsets[i] : i * a.stride;
     if (MODE == 0) {
         // a span outside [base, base + base_bytes) is not read (out = 0, counted)
+        ItemDesc d;
         const uint32_t len = a.lens ? a.lens[i] : a.len;
         d.sane = off <= a.base_bytes && len <= a.base_bytes - off;
         d.p = a.base + (d.sane ? off : 0);
         d.len = d.sane ? len : 0u;
         d.aux = a.crc_in ? a.crc_in[i] : 0u;
-    } else {
-        // item header fields (memcached.h:613-636), ITEM_ntotal (:149-152):
-        // bytes 28..41 of the image from the two aligned pieces holding them
-        const uint8_t *it = a.base + off;
-        const bool hdr_ok = off + 48 <= a.base_bytes;
-        uint64_t f0 = 0, f1 = 0;  // image bytes 28..35, 36..43
-        if (hdr_ok) {
-            const uintptr_t x = (uintptr_t)(it + 28), q = x & ~(uintptr_t)15, q2 = (x + 13) & ~(uintptr_t)15;
-            const Piece v0 = ld_piece((const uint8_t *)q), v1 = ld_piece((const uint8_t *)q2);
-            const uint32_t sh = (uint32_t)(x - q);  // 0..15
-            const uint64_t w0 = v0.lo, w1 = v0.hi, w2 = q2 != q ? v1.lo : 0, w3 = q2 != q ? v1.hi : 0;
-            const uint64_t a0 = sh < 8 ? w0 : w1, a1 = sh < 8 ? w1 : w2, a2 = sh < 8 ? w2 : w3;
-            const uint32_t k = 8 * (sh & 7u);
-            f0 = k ? (a0 >> k) | (a1 << (64 - k)) : a0;
-            f1 = k ? (a1 >> k) | (a2 << (64 - k)) : a1;
-        }
-        const uint32_t nbytes = (uint32_t)(f0 >> 32);
-        const uint32_t flags = (uint32_t)(f1 >> 16) & 0xffffu;
-        const uint32_t nkey = (uint32_t)(f1 >> 40) & 0xffu;
-        const uint64_t ntotal = 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) + ((flags & 2u) ? 8 : 0);
-        d.aux = (uint32_t)f0;
-        // an item never crosses its write buffer (extstore.c:627-636), so a
-        // header claiming otherwise is corrupt
-        const bool in_region = a.region == 0 || off / a.region == (off + ntotal - 1) / a.region;
-        d.sane = hdr_ok && nkey != 0 && nbytes < 0x80000000u && off + ntotal <= a.base_bytes && in_region;
-        d.p = it + 32;
-        d.len = d.sane ? (uint32_t)(ntotal - 32) : 0u;
+        return d;
     }
-    return d;
+    const bool hdr_ok = off + 48 <= a.base_bytes;
+    ItemHdr h{0u, 0u, 0u, 0u};
+    if (hdr_ok) h = parse_hdr(a.base + off);
+    return item_desc(a, off, h, hdr_ok);
 }
 
 // Work-unit record written by k_expand (32 B, one dwordx4 pair per unit):
@@ -1147,29 +1165,33 @@ __device__ __forceinline__ uint32_t span_units(const uint8_t *p, uint32_t len) {
 // the span's item record with its z (the header is parsed once per launch, and
 // the foreign bytes of the head and tail pieces are read here: for packed
 // images they share lines with the headers this pass reads anyway).
+// Span i's plan entries: one-block flag, unit count, item record, R = 0.
+template <int MODE>
+__device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const ItemDesc &it, const Tab8 &t8,
+                                           uint32_t *nunit, uint4 *irec, uint8_t *fast) {
+    // a span whose unit is one whole block goes to k_blocks (no units)
+    const uint8_t *g1;
+    bool none;
+    const bool one = it.sane && one_block(it.p, it.len, &g1, &none) && !none;
+    fast[i] = one;
+    nunit[i] = one ? 0u : span_units(it.p, it.len);
+    const uint64_t off = (uint64_t)(it.p - a.base);
+    uint32_t z = 0;
+    if (it.sane) {
+        z = span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow);
+        if (MODE == 1) z ^= t8.zeros(~it.aux, tail_pad(it.p, it.len));  // W
+    }
+    irec[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32) | (it.sane ? 0u : kInsane), it.len, z);
+    a.span_acc[i] = 0u;
+}
+
 template <int MODE>
 __global__ void k_count(SpanArgs a, uint32_t *nunit, uint4 *irec, uint8_t *fast) {
     __shared__ uint32_t s8[kTab8Dwords];
     const Tab8 t8 = load_tab8(s8, a.tab8);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x)
-    {
-        const ItemDesc it = fetch_item<MODE>(a, i);
-        // a span whose unit is one whole block goes to k_blocks (no units)
-        const uint8_t *g1;
-        bool none;
-        const bool one = it.sane && one_block(it.p, it.len, &g1, &none) && !none;
-        fast[i] = one;
-        nunit[i] = one ? 0u : span_units(it.p, it.len);
-        const uint64_t off = (uint64_t)(it.p - a.base);
-        uint32_t z = 0;
-        if (it.sane) {
-            z = span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow);
-            if (MODE == 1) z ^= t8.zeros(~it.aux, tail_pad(it.p, it.len));  // W
-        }
-        irec[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32) | (it.sane ? 0u : kInsane), it.len, z);
-        a.span_acc[i] = 0u;
-    }
+        count_item<MODE>(a, i, fetch_item<MODE>(a, i), t8, nunit, irec, fast);
 }
 
 // Write the unit records of span i at prefix[i].  Spans whose units would pass
@@ -1540,74 +1562,90 @@ __global__ void k_chain(const uint32_t *iov_crc, const uint32_t *lens, uint32_t 
 // Device-side page walk (storage_compact_readback, storage.c:950-1070): the
 // buffer is a sequence of wbuf-sized reads; in each, items are packed from
 // offset 0, nkey == 0 ends the wbuf, the next item is at + ITEM_ntotal, and the
-// walk stops when fewer than sizeof(item) = 48 bytes remain.  One thread per
-// wbuf (the walk is a dependent chain; a round trip fetches kWalkSpec headers
-// at the last item's stride, one round trip per kWalkSpec equal-sized items).
-//   k_walk (slots != nullptr): count the items of wbuf w into cnt[w] and keep
-//     the first kWalkSlots offsets (relative to the wbuf) in slots[w][];
-//   k_walk_place: copy the kept offsets to offs[prefix[w] + i];
-//   k_walk (slots == nullptr, prefix != nullptr): re-walk only the wbufs that
-//     held more than kWalkSlots items, writing offsets >= kWalkSlots.
-constexpr uint32_t kWalkSlots = 2048;
-#ifndef MCRC_WALK_SPEC
-#define MCRC_WALK_SPEC 8
+// walk stops when fewer than sizeof(item) = 48 bytes remain.  Two passes:
+//   k_walk<false>: count the items of wbuf w into cnt[w];
+//   (exclusive scan of the counts: prefix[w] = the index of wbuf w's first item)
+//   k_walk<true>: walk again and write item prefix[w] + c's offset and, for a
+//     planned verify, its plan entries (count_item: what k_count would write
+//     after reading the header a second time), so no k_count pass follows.
+// One wave per wbuf.  The walk is a dependent chain, so each round trip
+// guesses: lane j reads the header at off + j * s, s = the last item's
+// ITEM_ntotal.  Lane j's guess is right iff every lane before it holds an item
+// of exactly s bytes; the first lane m where that fails (a ballot) still sits
+// on a true item boundary, so lanes [0, m) are items, lane m is one too unless
+// it ends the wbuf (nkey == 0, or fewer than 48 bytes left), and the walk goes
+// on from lane m's item end with s = its ntotal.  Whatever the data, the
+// result is the sequential walk's (tests/test_walk_model.py restates it);
+// equal-sized items cost one round trip per 64 of them.
+#ifndef MCRC_WALK_WAVES
+#define MCRC_WALK_WAVES 4
 #endif
-constexpr int kWalkSpec = MCRC_WALK_SPEC;  // headers fetched per round trip (stride prediction)
+constexpr uint32_t kWalkWaves = MCRC_WALK_WAVES;  // waves (wbufs) per workgroup
 
-__global__ void k_walk(const uint8_t *base, uint64_t bytes, uint64_t wbuf, uint64_t nw, uint32_t *cnt,
-                       uint32_t *slots, const uint32_t *prefix, uint64_t *offs) {
-    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nw;
-         w += (uint64_t)gridDim.x * blockDim.x) {
-        if (!slots && cnt[w] <= kWalkSlots) continue;  // second pass: overflowed wbufs only
-        const uint64_t start = w * wbuf, size = bytes - start < wbuf ? bytes - start : wbuf;
-        uint64_t off = 0, s = 0;  // s: stride of the last item walked
-        uint32_t c = 0;
-        bool done = false;
-        while (!done && off + 48 <= size) {
-            // One round trip fetches the headers at off, off + s, off + 2s, ...
-            // (the last stride predicts the next ones).  A predicted header is
-            // used only when the walk, recomputed from the real fields, lands on
-            // it, so the result is the sequential walk's whatever the data.
-            uint32_t nkey[kWalkSpec], nbytes[kWalkSpec], flags[kWalkSpec];
-#pragma unroll
-            for (int j = 0; j < kWalkSpec; ++j) {
-                const uint64_t o = off + j * s;
-                nkey[j] = nbytes[j] = flags[j] = 0;
-                if (j == 0 || (s != 0 && o + 48 <= size)) {
-                    const uint8_t *it = base + start + o;
-                    nkey[j] = it[41];
-                    nbytes[j] = ld_u32_unaligned(it + 32);
-                    flags[j] = it[38] | (it[39] << 8);
-                }
+struct WalkOut {
+    uint32_t *cnt;           // count pass: items per wbuf
+    const uint32_t *prefix;  // emit pass: index of each wbuf's first item
+    uint64_t *offs;          // emit pass: item offsets from base
+    uint32_t *nunit;         // emit pass, planned verify (else nullptr): k_count's entries
+    uint4 *irec;
+    uint8_t *fast;
+};
+
+// a: base, base_bytes (the walked bytes), region (= wbuf), and for the plan
+// entries xpow, tab8, span_acc.
+template <bool EMIT>
+__global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t nw, WalkOut out) {
+    __shared__ uint32_t s8[EMIT ? kTab8Dwords : 1];
+    Tab8 t8{s8};
+    const bool plan = EMIT && out.irec;
+    if (plan) t8 = load_tab8(s8, a.tab8);
+    const uint32_t j = threadIdx.x & 63u;
+    const uint64_t wbuf = a.region;
+    // the wave's wbuf index as a scalar: the walk state (off, s, c) is then
+    // wave-uniform in the compiler's view too, and the loops are scalar loops
+    // (with the index in a VGPR the walk went wrong on large page sets)
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t w = (uint64_t)blockIdx.x * kWalkWaves + wave; w < nw; w += (uint64_t)gridDim.x * kWalkWaves) {
+        const uint64_t start = w * wbuf, size = a.base_bytes - start < wbuf ? a.base_bytes - start : wbuf;
+        const uint8_t *wb = a.base + start;
+        const uint64_t first = EMIT ? out.prefix[w] : 0;
+        uint64_t off = 0, s = 0;  // wave-uniform: next item, stride guess (0: none yet)
+        uint32_t c = 0;           // items walked so far
+        while (off + 48 <= size) {
+            const uint64_t o = off + j * s;
+            const bool in = (j == 0 || s != 0) && o + 48 <= size;  // (s < 2^33: no overflow)
+            ItemHdr h{0u, 0u, 0u, 0u};
+            if (in) h = parse_hdr(wb + o);
+            const uint64_t nt = h.ntotal();
+            const bool item = in && h.nkey != 0;
+            // m = the first lane whose successor's guess is wrong (64: none)
+            const uint64_t brk = __ballot(!(item && nt == s));
+            const uint32_t m = brk ? (uint32_t)__ffsll((unsigned long long)brk) - 1u : 64u;
+            // lane m (if any) is on a true boundary: an item, or the end of the wbuf
+            bool last_item = false;
+            uint64_t nt_m = 0;
+            if (m < 64u) {  // (m is wave-uniform: scalar reads of lane m)
+                last_item = __builtin_amdgcn_readlane((int)item, (int)m) != 0;
+                nt_m = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)nt, (int)m) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(nt >> 32), (int)m) << 32);
             }
-            const uint64_t o0 = off, s0 = s;
-#pragma unroll
-            for (int j = 0; j < kWalkSpec; ++j) {
-                if (j > 0 && (s0 == 0 || off != o0 + j * s0)) break;  // prediction missed: reload at off
-                if (off + 48 > size || nkey[j] == 0) {  // end of the wbuf / zeroed tail
-                    done = true;
-                    break;
-                }
-                if (slots) {
-                    if (c < kWalkSlots) slots[w * kWalkSlots + c] = (uint32_t)off;
-                } else if (c >= kWalkSlots) {
-                    offs[prefix[w] + c] = start + off;
-                }
-                ++c;
-                s = 48ull + nkey[j] + 1 + nbytes[j] + ((flags[j] & 256u) ? 4 : 0) + ((flags[j] & 2u) ? 8 : 0);
-                off += s;
+            const uint32_t k = m < 64u ? m + (last_item ? 1u : 0u) : 64u;  // items this round trip
+            if (EMIT && j < k) {
+                const uint64_t i = first + c + j;
+                out.offs[i] = start + o;
+                if (plan) count_item<1>(a, i, item_desc(a, start + o, h, true), t8, out.nunit, out.irec, out.fast);
+            }
+            c += k;
+            if (m == 64u) {
+                off += 64u * s;
+            } else if (!last_item) {
+                break;  // lane m ends the wbuf
+            } else {
+                off += m * s + nt_m;
+                s = nt_m;
             }
         }
-        if (slots) cnt[w] = c;
-    }
-}
-
-__global__ void k_walk_place(uint64_t wbuf, uint64_t nw, const uint32_t *cnt, const uint32_t *slots,
-                             const uint32_t *prefix, uint64_t *offs) {
-    for (uint64_t w = blockIdx.x; w < nw; w += gridDim.x) {
-        const uint32_t c = cnt[w] < kWalkSlots ? cnt[w] : kWalkSlots;
-        for (uint32_t i = threadIdx.x; i < c; i += blockDim.x)
-            offs[prefix[w] + i] = w * wbuf + slots[w * kWalkSlots + i];
+        if (!EMIT && j == 0) out.cnt[w] = c;
     }
 }
 

@@ -128,7 +128,7 @@ struct Device {
         return s.p;
     }
 };
-enum { kScrWalkCnt, kScrWalkCnt1, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage, kScrWalkSlots };
+enum { kScrWalkCnt, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage };
 
 std::mutex g_dev_mu;
 std::vector<std::unique_ptr<Device>> g_devs;
@@ -328,8 +328,26 @@ uint64_t small_max() {
     return e ? std::min<uint64_t>(strtoull(e, nullptr, 10), mcrc_dev::kSmallMax) : mcrc_dev::kSmallMax;
 }
 
+// One launch (k_small) for small batches whose spans are bounded: a group
+// reads its whole span alone, so a batch of a few multi-MiB spans is left to
+// the planned path (segments over the whole grid).
 template <int MODE>
-int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) {
+bool takes_small(const mcrc_dev::SpanArgs &a) {
+    const bool bounded = MODE == 0 && a.lens == nullptr ? a.len <= kSmallSpanMax : a.base_bytes <= kSmallBaseMax;
+    return a.n <= small_max() && bounded;
+}
+
+// Unit capacity of a planned batch: units fit whenever the spans do not
+// overlap; overlapping long spans past it are processed whole by the second
+// span pass.
+uint64_t plan_cap(const mcrc_dev::SpanArgs &a) {
+    return std::min<uint64_t>(a.n + a.base_bytes / mcrc_dev::kSegBytes + 1 + a.n / 4096, 0xfffffff0ull);
+}
+
+// counted: the plan entries of k_count (unit counts, item records, one-block
+// flags, zeroed accumulators) are already written (the page walk's second pass).
+template <int MODE>
+int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st, bool counted = false) {
     const uint64_t n = a.n;
     const bool identity = MODE == 0 && a.lens == nullptr && a.len <= mcrc_dev::kSegBytes;
     (void)aligned;
@@ -346,11 +364,7 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
     // groups cost 30 us of same-address atomics per 4.8 M verified items, 64 Ki
     // groups 190 us); k_count: 4096 (1024 measured 25 % slower on config 3).
     const int gf = (int)std::min<uint64_t>((n + 255) / 256, 1024);
-    // One launch (k_small) for small batches whose spans are bounded: a group
-    // reads its whole span alone, so a batch of a few multi-MiB spans is
-    // left to the planned path (segments over the whole grid).
-    const bool bounded = MODE == 0 && a.lens == nullptr ? a.len <= kSmallSpanMax : a.base_bytes <= kSmallBaseMax;
-    if (n <= small_max() && bounded) {
+    if (!counted && takes_small<MODE>(a)) {
         hipLaunchKernelGGL((mcrc_dev::k_small<MODE>), dim3((unsigned)((n + 31) / 32)), dim3(1024),
                            mcrc_dev::kLdsImageK1Bytes, st, a, d.img);
         HIP_OK(hipGetLastError());
@@ -375,16 +389,15 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st) 
         return CRC32C_OK;
     }
     if (n >= 0xffffffffull) return CRC32C_EINVAL;
-    // units fit in cap whenever the spans do not overlap; overlapping long spans
-    // past cap are processed whole by the second span pass
-    const uint64_t cap = std::min<uint64_t>(n + a.base_bytes / mcrc_dev::kSegBytes + 1 + n / 4096, 0xfffffff0ull);
+    const uint64_t cap = plan_cap(a);
     int rc = ensure_plan(d, n, cap);
     if (rc) return rc;
     uint32_t *nvalid = d.counters, *nwhole = d.counters + 1, *nbig = d.counters + 2, *nfast = d.counters + 3;
     HIP_OK(hipMemsetAsync(nvalid, 0xff, 4, st));
     HIP_OK(hipMemsetAsync(nwhole, 0, 8, st));  // nwhole, nbig
     a.span_acc = d.span_acc;
-    hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nunit, d.irec, d.fast);
+    if (!counted)
+        hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nunit, d.irec, d.fast);
     size_t tmp = d.scan_tmp_bytes;
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(d.scan_tmp, tmp, d.nunit, d.prefix, (int)n, st));
     tmp = d.scan_tmp_bytes;
@@ -905,29 +918,29 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
         HIP_OK(hipMemcpyAsync(b, base, base_bytes, hipMemcpyHostToDevice, st));
         dbase = b;
     }
-    uint32_t *cnt = (uint32_t *)d->grow(kScrWalkCnt, nw * 4);
+    // counts of nw wbufs and a zero: the exclusive scan's last entry is the total
+    uint32_t *cnt = (uint32_t *)d->grow(kScrWalkCnt, (nw + 1) * 4);
     uint32_t *prefix = (uint32_t *)d->grow(kScrWalkPrefix, (nw + 1) * 4);
     size_t tmp = 0;
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, prefix, (int)nw + 1));
     void *scan = d->grow(kScrWalkScan, tmp);
     if (!cnt || !prefix || !scan) return CRC32C_ENOMEM;
-    // one walking thread per wbuf, 16 per workgroup: a page's walks spread over
-    // every CU (256-thread groups put 1000 pages' walks on 63 CUs)
-#ifndef MCRC_WALK_BLOCK
-#define MCRC_WALK_BLOCK 16
-#endif
-    constexpr int kWalkBlock = MCRC_WALK_BLOCK;
-    const int gw = (int)std::min<uint64_t>((nw + kWalkBlock - 1) / kWalkBlock, 65535);
-    uint32_t *slots = (uint32_t *)d->grow(kScrWalkSlots, nw * mcrc_dev::kWalkSlots * 4);
-    if (!slots) return CRC32C_ENOMEM;
-    hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(kWalkBlock), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt, slots,
-                       (const uint32_t *)nullptr, (uint64_t *)nullptr);
-    // prefix[nw] = total: scan nw + 1 counts with a zero appended
-    uint32_t *cnt1 = (uint32_t *)d->grow(kScrWalkCnt1, (nw + 1) * 4);
-    if (!cnt1) return CRC32C_ENOMEM;
-    HIP_OK(hipMemcpyAsync(cnt1, cnt, nw * 4, hipMemcpyDeviceToDevice, st));
-    HIP_OK(hipMemsetAsync(cnt1 + nw, 0, 4, st));
-    HIP_OK(hipcub::DeviceScan::ExclusiveSum(scan, tmp, cnt1, prefix, (int)nw + 1, st));
+    mcrc_dev::SpanArgs a{};
+    a.base = dbase;
+    a.base_bytes = base_bytes;
+    a.nbad = d->nbad;
+    a.xpow = d->xpow;
+    a.tab8 = d->tab8;
+    a.zero = d->zero;
+    a.region = wbuf_bytes;
+    // one walking wave per wbuf, kWalkWaves per workgroup
+    const int gw = (int)std::min<uint64_t>((nw + mcrc_dev::kWalkWaves - 1) / mcrc_dev::kWalkWaves, 65535);
+    const dim3 bw(64 * mcrc_dev::kWalkWaves);
+    mcrc_dev::WalkOut wo{};
+    wo.cnt = cnt;
+    HIP_OK(hipMemsetAsync(cnt + nw, 0, 4, st));
+    hipLaunchKernelGGL(mcrc_dev::k_walk<false>, dim3(gw), bw, 0, st, a, nw, wo);
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(scan, tmp, cnt, prefix, (int)nw + 1, st));
     uint32_t total = 0;
     HIP_OK(hipMemcpyAsync(&total, prefix + nw, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -940,23 +953,25 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     uint64_t *doffs = direct ? offsets : (uint64_t *)d->grow(kScrWalkOffs, (size_t)total * 8);
     uint8_t *dok = direct ? ok : (uint8_t *)d->grow(kScrWalkOk, total);
     if (!doffs || !dok) return CRC32C_ENOMEM;
-    hipLaunchKernelGGL(mcrc_dev::k_walk_place, dim3((int)std::min<uint64_t>(nw, 8192)), dim3(256), 0, st, wbuf_bytes,
-                       nw, (const uint32_t *)cnt, (const uint32_t *)slots, (const uint32_t *)prefix, doffs);
-    hipLaunchKernelGGL(mcrc_dev::k_walk, dim3(gw), dim3(kWalkBlock), 0, st, dbase, base_bytes, wbuf_bytes, nw, cnt,
-                       (uint32_t *)nullptr, (const uint32_t *)prefix, doffs);
-    mcrc_dev::SpanArgs a{};
-    a.base = dbase;
-    a.base_bytes = base_bytes;
     a.offsets = doffs;
     a.ok = dok;
-    a.nbad = d->nbad;
     a.n = total;
-    a.xpow = d->xpow;
-    a.tab8 = d->tab8;
-    a.zero = d->zero;
-    a.region = wbuf_bytes;
+    // the second walk writes the offsets and, for a planned verify, the plan
+    // entries k_count would make (the headers are read once more, not twice)
+    const bool planned = !takes_small<1>(a);
+    if (planned) {
+        rc = ensure_plan(*d, total, plan_cap(a));
+        if (rc) return rc;
+        a.span_acc = d->span_acc;
+    }
+    wo.prefix = prefix;
+    wo.offs = doffs;
+    wo.nunit = planned ? d->nunit : nullptr;
+    wo.irec = planned ? d->irec : nullptr;
+    wo.fast = planned ? d->fast : nullptr;
+    hipLaunchKernelGGL(mcrc_dev::k_walk<true>, dim3(gw), bw, 0, st, a, nw, wo);
     HIP_OK(hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st));
-    rc = launch_units<1>(*d, a, false, st);
+    rc = launch_units<1>(*d, a, false, st, /*counted=*/planned);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     const uint64_t k = std::min<uint64_t>(cap, total);

@@ -303,7 +303,7 @@ def _walk(buf, wbuf):
         size, off = min(wbuf, buf.size - start), 0
         while off + 48 <= size and buf[start + off + 41] != 0:
             offs.append(start + off)
-            off += layout.ntotal_of(buf, start + off)
+            off += layout.ntotal_of(buf, start + off) & 0xffffffff  # (unsigned int ntotal, storage.c:954)
     return np.asarray(offs, np.uint64)
 
 
@@ -374,6 +374,63 @@ def test_verify_pages_walk_stride_runs(torch):
     got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, buf), 256 << 10)
     np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), offs)
     assert nbad == int((got_ok.cpu().numpy() == 0).sum())
+
+
+def test_verify_pages_walk_wave_runs(torch):
+    """The walk reads 64 guessed headers per round trip (one wave per wbuf):
+    runs of equal items just under, at and over the wave width, wbufs that end
+    inside or right after a run, and corrupt sizes mid-run walk exactly as
+    storage.c:950-1070 (tests/test_walk_model.py restates the round trip)."""
+    rng = np.random.default_rng(44)
+    sizes = []
+    for run in (63, 64, 65, 1, 128, 129, 127, 2, 300, 64, 64, 5):
+        sizes += [int(rng.choice([0, 3, 100, 4096]))] * run
+    items = [layout.make_item(b"v%06d" % i, rng.integers(0, 256, n, dtype=np.uint8).tobytes(), cas=i + 1)
+             for i, n in enumerate(sizes)]
+    for wbuf in (1 << 20, 4165 * 64 + 47, 4165 * 64 + 48, 4165 * 128):
+        buf, offs = layout.pack_wbufs(items, wbuf)
+        want = _walk(buf, wbuf)
+        np.testing.assert_array_equal(want, offs)
+        for flip in (None, 33, 35, 41):
+            b = buf.copy()
+            if flip is not None:
+                b[int(offs[int(rng.integers(0, offs.size))]) + flip] ^= np.uint8(0x80 if flip == 35 else 0x01)
+            got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, b), wbuf)
+            np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), _walk(b, wbuf))
+
+
+def test_verify_pages_bench_layout(torch):
+    """The bench's config-5 pages (4 x 64 MiB, 1007 packed 4165-B images per
+    4 MiB wbuf, 1 % single-bit flips) plus flipped header bits (nbytes,
+    it_flags, nkey) in 40 images: the planned device walk + verify gives the
+    sequential walk's items and the oracle's verdicts, leaves the pages
+    untouched, and gives the same answer when repeated."""
+    import argparse
+    import bench
+    bench.workload_config5(argparse.Namespace(pages=4), 0, 1)
+    data = bench._KEEP[-2]
+    buf = data.cpu().numpy()
+    rng = np.random.default_rng(45)
+    for it in rng.choice(4 * 16 * 1007, 40, replace=False):
+        o = int(it // 1007) * (4 << 20) + int(it % 1007) * 4165
+        buf[o + int(rng.choice([32, 33, 34, 35, 38, 39, 41]))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    want = _walk(buf, 4 << 20)
+    d = _dev(torch, buf)
+    for rep in range(2):
+        got_offs, got_ok, nbad = mc.verify_pages(d, 4 << 20)
+        got_offs = got_offs.cpu().numpy().astype(np.uint64)
+        np.testing.assert_array_equal(got_offs, want)
+        np.testing.assert_array_equal(d.cpu().numpy(), buf)
+    # the verdicts: the stored CRC of every item whose span is sane
+    spans_ok = []
+    for o in want:
+        o = int(o)
+        nt = layout.ntotal_of(buf, o) & 0xffffffff
+        sane = buf[o + 41] != 0 and o + nt <= buf.size and o // (4 << 20) == (o + nt - 1) // (4 << 20)
+        spans_ok.append(bool(sane) and oracle.crc32c(0, buf[o + 32:o + nt]) ==
+                        int(buf[o + 28:o + 32].view(np.uint32)[0]))
+    np.testing.assert_array_equal(got_ok.cpu().numpy().astype(bool), np.array(spans_ok))
+    assert nbad == len(spans_ok) - int(np.sum(spans_ok))
 
 
 def test_chained_iovs(torch):

@@ -1,0 +1,110 @@
+"""CPU check of the device page walk's round-trip algebra (k_walk in
+crc32c_kernels.hip, restated here): one wave per wbuf guesses that the next 64
+items all have the last item's size, reads their headers in one round trip,
+and keeps the guesses up to the first lane whose item breaks the run.  The
+claim to check is that this gives exactly the sequential walk of
+storage_compact_readback (storage.c:950-1070) for ANY bytes: runs of equal
+sizes of every length around the wave width, runs broken by other sizes, a
+zeroed nkey, corrupt sizes, wbufs ending a few bytes after an item.  No GPU
+needed."""
+import numpy as np
+import pytest
+
+from memcached_amd import layout
+
+WAVE = 64
+
+
+def ntotal(buf, off):
+    """ITEM_ntotal as the kernels compute it (ItemHdr::ntotal): nbytes as an
+    unsigned 32-bit field, the sum in 64 bits (a corrupt size ends the wbuf
+    instead of stepping backwards)."""
+    nbytes = int.from_bytes(bytes(buf[off + 32:off + 36]), "little")
+    flags = int(buf[off + 38]) | int(buf[off + 39]) << 8
+    return 48 + int(buf[off + 41]) + 1 + nbytes + (4 if flags & 256 else 0) + (8 if flags & 2 else 0)
+
+
+def seq_walk(buf, start, size):
+    """storage.c:950-1070: nkey == 0 or fewer than 48 bytes left ends the wbuf."""
+    out, off = [], 0
+    while off + 48 <= size and buf[start + off + 41] != 0:
+        out.append(off)
+        off += ntotal(buf, start + off)
+    return out
+
+
+def wave_walk(buf, start, size):
+    """k_walk's loop, lane by lane (returns the offsets and the round trips)."""
+    out, off, s, trips = [], 0, 0, 0
+    while off + 48 <= size:
+        trips += 1
+        lanes = []
+        for j in range(WAVE):
+            o = off + j * s
+            inb = (j == 0 or s != 0) and o + 48 <= size
+            nkey = int(buf[start + o + 41]) if inb else 0
+            nt = ntotal(buf, start + o) if inb else 48 + 1  # (header of zeros)
+            item = inb and nkey != 0
+            lanes.append((o, item, nt))
+        m = next((j for j, (_o, item, nt) in enumerate(lanes) if not (item and nt == s)), WAVE)
+        last_item = m < WAVE and lanes[m][1]
+        k = m + (1 if last_item else 0) if m < WAVE else WAVE
+        out += [lanes[j][0] for j in range(k)]
+        if m == WAVE:
+            off += WAVE * s
+        elif not last_item:
+            break
+        else:
+            off += m * s + lanes[m][2]
+            s = lanes[m][2]
+    return out, trips
+
+
+def _pages(rng, sizes, wbuf, cut=0):
+    items = [layout.make_item(b"w%06d" % i, rng.integers(0, 256, n, dtype=np.uint8).tobytes(), cas=i + 1)
+             for i, n in enumerate(sizes)]
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    return buf[:buf.size - cut] if cut else buf
+
+
+def _check(buf, wbuf):
+    for start in range(0, buf.size, wbuf):
+        size = min(wbuf, buf.size - start)
+        got, _ = wave_walk(buf, start, size)
+        assert got == seq_walk(buf, start, size)
+
+
+@pytest.mark.parametrize("run", [1, 2, 63, 64, 65, 127, 128, 129, 300])
+def test_equal_runs(run):
+    rng = np.random.default_rng(run)
+    sizes = []
+    while len(sizes) < 900:
+        sizes += [int(rng.choice([0, 5, 100, 4096]))] * run
+    for wbuf in (1 << 20, 4165 * 64 + 47, 4165 * 64 + 48, 4165 * 65):
+        _check(_pages(rng, sizes, wbuf, cut=wbuf // 3), wbuf)
+
+
+def test_corrupt_headers():
+    """Flipped nbytes bits (huge or odd sizes), zeroed nkeys and random header
+    bytes: the walk goes wherever the sequential walk goes."""
+    rng = np.random.default_rng(7)
+    wbuf = 1 << 20
+    buf = _pages(rng, [4096] * 600 + [int(x) for x in rng.integers(0, 3000, 400)], wbuf)
+    offs = seq_walk(buf, 0, min(wbuf, buf.size))
+    for t in range(40):
+        b = buf.copy()
+        for o in rng.choice(offs, 3, replace=False):
+            pos = int(o) + int(rng.choice([32, 33, 34, 35, 38, 39, 41]))
+            b[pos] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        if t % 4 == 0:
+            b[int(offs[int(rng.integers(0, len(offs)))]) + 41] = 0
+        _check(b, wbuf)
+
+
+def test_round_trips():
+    """Equal-sized items cost one round trip per 64 (plus the first)."""
+    rng = np.random.default_rng(3)
+    wbuf = 4 << 20
+    buf = _pages(rng, [4096] * 1007, wbuf)
+    got, trips = wave_walk(buf, 0, wbuf)
+    assert len(got) == 1007 and trips == 1 + -(-1006 // WAVE) + (1 if 1006 % WAVE == 0 else 0)
