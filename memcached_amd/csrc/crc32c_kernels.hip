@@ -747,10 +747,13 @@ struct ItemHdr {
     }
 };
 __device__ __forceinline__ ItemHdr parse_hdr(const uint8_t *it) {
-    const uintptr_t x = (uintptr_t)(it + 28), q = x & ~(uintptr_t)15, q2 = (x + 13) & ~(uintptr_t)15;
-    const Piece v0 = ld_piece((const uint8_t *)q), v1 = ld_piece((const uint8_t *)q2);
-    const uint32_t sh = (uint32_t)(x - q);  // 0..15
-    const uint64_t w0 = v0.lo, w1 = v0.hi, w2 = q2 != q ? v1.lo : 0, w3 = q2 != q ? v1.hi : 0;
+    // (pointer arithmetic, not an integer round trip: the loads stay global
+    // loads instead of flat ones, which would also count in lgkmcnt)
+    const uint32_t sh = (uint32_t)((uintptr_t)(it + 28) & 15u);  // 0..15
+    const uint8_t *q = it + 28 - sh;
+    const bool two = sh + 13 >= 16;  // byte 41 lies in the next piece
+    const Piece v0 = ld_piece(q), v1 = ld_piece(q + (two ? 16 : 0));
+    const uint64_t w0 = v0.lo, w1 = v0.hi, w2 = two ? v1.lo : 0, w3 = two ? v1.hi : 0;
     const uint64_t a0 = sh < 8 ? w0 : w1, a1 = sh < 8 ? w1 : w2, a2 = sh < 8 ? w2 : w3;
     const uint32_t k = 8 * (sh & 7u);
     const uint64_t f0 = k ? (a0 >> k) | (a1 << (64 - k)) : a0;  // image bytes 28..35
