@@ -968,11 +968,9 @@ __device__ __forceinline__ void emit(const SpanArgs &a, uint64_t item, uint32_t 
         if (a.out) {
             a.out[item] = crc;
         } else {
-            uint8_t *x = const_cast<uint8_t *>(p) - 4;
-            x[0] = (uint8_t)crc;
-            x[1] = (uint8_t)(crc >> 8);
-            x[2] = (uint8_t)(crc >> 16);
-            x[3] = (uint8_t)(crc >> 24);
+            // one dword store at any alignment (global memory takes unaligned
+            // stores on gfx950; the compiler emits that for this memcpy)
+            __builtin_memcpy(const_cast<uint8_t *>(p) - 4, &crc, 4);
         }
     }
 }
@@ -1624,14 +1622,15 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
             // m = the first lane whose successor's guess is wrong (64: none)
             const uint64_t brk = __ballot(!(item && nt == s));
             const uint32_t m = brk ? (uint32_t)__ffsll((unsigned long long)brk) - 1u : 64u;
-            // lane m (if any) is on a true boundary: an item, or the end of the wbuf
-            bool last_item = false;
-            uint64_t nt_m = 0;
-            if (m < 64u) {  // (m is wave-uniform: scalar reads of lane m)
-                last_item = __builtin_amdgcn_readlane((int)item, (int)m) != 0;
-                nt_m = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)nt, (int)m) |
-                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(nt >> 32), (int)m) << 32);
-            }
+            // lane m (if any) is on a true boundary: an item, or the end of the
+            // wbuf.  Its flag and size are broadcast to every lane (ds_bpermute),
+            // and the walk state stays in VGPRs, equal in all lanes: with it in
+            // SGPRs from readlane the walk went wrong on large page sets (the
+            // same ISA read correct by hand)
+            const int src = m < 64u ? (int)m : 0;
+            const bool last_item = m < 64u && __shfl((int)item, src, 64) != 0;
+            const uint64_t nt_m = (uint64_t)(uint32_t)__shfl((int)(uint32_t)nt, src, 64) |
+                                  ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(nt >> 32), src, 64) << 32);
             const uint32_t k = m < 64u ? m + (last_item ? 1u : 0u) : 64u;  // items this round trip
             if (EMIT && j < k) {
                 const uint64_t i = first + c + j;
