@@ -214,6 +214,9 @@ def zipf_lens(n: int, seed: int = 7):
     return np.clip(classes[k] + rng.uniform(-step, step), 1, 1 << 20).astype(np.uint32)
 
 
+_KEEP = []  # device tensors whose raw pointers a workload hands to the library
+
+
 def workload_config3(args, rank, world):
     """1 Mi spans of Zipf sizes packed back to back at odd offsets (K2)."""
     import numpy as np
@@ -227,6 +230,7 @@ def workload_config3(args, rank, world):
     out = torch.empty(lens.size, dtype=torch.int32, device="cuda")
     spans = _lib.Spans(data.data_ptr(), total, d_offs.data_ptr(), 0, d_lens.data_ptr(), 0, None, out.data_ptr(),
                        lens.size)
+    _KEEP.extend((data, d_offs, d_lens, out))  # the raw pointers in spans must outlive this frame
     return spans, int(lens.astype(np.uint64).sum()), {
         "workload": "BASELINE configs[2]: 1 Mi spans, Zipf sizes 64 B - 1 MiB (44 classes, s = 1), packed "
                     "back to back at odd offsets, K2 k_spans<unaligned>",
@@ -244,9 +248,6 @@ def run_verify_steps(args_v, steps: int, stream):
                                                 _lib.CRC32C_DEVICE, ctypes.c_void_p(stream.cuda_stream)))
         b.record(stream)
     return evs, int(nbad.value)
-
-
-_KEEP = []  # device tensors whose raw pointers a workload hands to the library
 
 
 def workload_config5(args, rank, world):

@@ -234,9 +234,28 @@ __device__ __forceinline__ uint32_t group_reduce32_span(uint32_t v, uint32_t lan
 }
 
 // Copy a table image from global memory into this workgroup's LDS.
+// (A thread's loads are all issued before its LDS stores: one load, wait and
+// store per iteration made the 160 KiB copy ten dependent L2 round trips per
+// workgroup.)
 __device__ __forceinline__ void load_tables(char *lds, const uint4 *__restrict__ img, uint32_t bytes) {
     uint4 *dst = reinterpret_cast<uint4 *>(lds);
-    for (uint32_t i = threadIdx.x; i < bytes / 16; i += blockDim.x) dst[i] = img[i];
+    const uint32_t n = bytes / 16;
+#ifdef MCRC_TABLES_SERIAL  // (ablation: the one-load-per-iteration copy)
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = img[i];
+    __syncthreads();
+    return;
+#endif
+    constexpr uint32_t U = 10;  // 160 KiB / (1024 threads x 16 B)
+    for (uint32_t i0 = threadIdx.x; i0 < n; i0 += U * blockDim.x) {
+        uint4 v[U];
+        // (indices clamped, not predicated: under a branch each load would be
+        // sunk to its store and waited for at once; a clamped thread rewrites
+        // the last entry with its own value)
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) v[u] = img[min(i0 + u * blockDim.x, n - 1)];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) dst[min(i0 + u * blockDim.x, n - 1)] = v[u];
+    }
     __syncthreads();
 }
 

@@ -603,8 +603,19 @@ struct Tab8 {
 };
 constexpr uint32_t kTab8Dwords = 20 * 256;  // 16 byte tables + the M_4096 operator, 20 KiB
 // (every thread of the block calls it)
+// (s: 16-B aligned; 16-B pieces, every load of a thread issued before its
+// stores, as load_tables)
 __device__ __forceinline__ Tab8 load_tab8(uint32_t *s, const uint32_t *tab8) {
-    for (uint32_t i = threadIdx.x; i < kTab8Dwords; i += blockDim.x) s[i] = tab8[i];
+    constexpr uint32_t n = kTab8Dwords / 4, U = 8;
+    uint4 *dst = reinterpret_cast<uint4 *>(s);
+    const uint4 *src = reinterpret_cast<const uint4 *>(tab8);
+    for (uint32_t i0 = threadIdx.x; i0 < n; i0 += U * blockDim.x) {
+        uint4 v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) v[u] = src[min(i0 + u * blockDim.x, n - 1)];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) dst[min(i0 + u * blockDim.x, n - 1)] = v[u];
+    }
     __syncthreads();
     return {s};
 }
@@ -1188,7 +1199,7 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
 
 template <int MODE>
 __global__ void k_count(SpanArgs a, uint32_t *nunit, uint4 *irec, uint8_t *fast) {
-    __shared__ uint32_t s8[kTab8Dwords];
+    __shared__ __attribute__((aligned(16))) uint32_t s8[kTab8Dwords];
     const Tab8 t8 = load_tab8(s8, a.tab8);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x)
@@ -1272,7 +1283,7 @@ __device__ __forceinline__ void count_bad(unsigned long long *nbad, uint32_t nb)
 //   one unit per span (MODE 0, no plan): R = out[i], Z computed here.
 template <int MODE, bool UNITS>
 __global__ void k_final(SpanArgs a, const uint4 *irec) {
-    __shared__ uint32_t s8[UNITS ? 1 : kTab8Dwords];
+    __shared__ __attribute__((aligned(16))) uint32_t s8[UNITS ? 1 : kTab8Dwords];
     Tab8 t8{s8};
     if (!UNITS) t8 = load_tab8(s8, a.tab8);
     uint32_t nb = 0;  // bad spans seen by this thread
@@ -1596,7 +1607,7 @@ struct WalkOut {
 // entries xpow, tab8, span_acc.
 template <bool EMIT>
 __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t nw, WalkOut out) {
-    __shared__ uint32_t s8[EMIT ? kTab8Dwords : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t s8[EMIT ? kTab8Dwords : 1];
     Tab8 t8{s8};
     const bool plan = EMIT && out.irec;
     if (plan) t8 = load_tab8(s8, a.tab8);

@@ -470,6 +470,36 @@ def test_verify_pages_bench_layout(torch, span_path, pages):
     assert nbad == len(spans_ok) - int(np.sum(spans_ok))
 
 
+def test_config3_full_size(torch, span_path):
+    """BASELINE config 3 at full size through the bench's own generator (1 Mi
+    Zipf spans of 64 B - 1 MiB at odd offsets, 28.5 GB): two runs agree on
+    every span, and 4000 spans (the 64 longest, the 64 shortest, the rest at
+    random) match the oracle."""
+    import argparse
+    import ctypes
+    import bench
+    if span_path == "small":
+        pytest.skip("a planned batch (1 Mi spans)")
+    spans, nbytes, _ = bench.workload_config3(argparse.Namespace(items=1 << 20), 0, 1)
+    data, d_offs, d_lens, out = bench._KEEP[-4:]
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(spans), _lib.CRC32C_DEVICE, None))
+    torch.cuda.synchronize()
+    first = out.clone()
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(spans), _lib.CRC32C_DEVICE, None))
+    torch.cuda.synchronize()
+    assert torch.equal(first, out)
+    offs, lens = d_offs.cpu().numpy().view(np.uint64), d_lens.cpu().numpy().view(np.uint32)
+    order = np.argsort(lens, kind="stable")
+    rng = np.random.default_rng(46)
+    pick = np.unique(np.concatenate([order[:64], order[-64:], rng.choice(lens.size, 3872, replace=False)]))
+    got = _u32(out)[pick]
+    for j, i in enumerate(pick):
+        o, n = int(offs[i]), int(lens[i])
+        assert got[j] == oracle.crc32c(0, data[o:o + n].cpu().numpy()), (int(i), n)
+    del data, d_offs, d_lens, out, first
+    bench._KEEP.clear()
+
+
 def test_chained_iovs(torch):
     """Chunked items (storage.c:163-170): the CRC chained over an item's iovs
     (header from +32, then each chunk) equals crc32c(0, concatenation)."""

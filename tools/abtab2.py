@@ -8,6 +8,7 @@ for f in sorted(glob.glob(os.path.join(sys.argv[1], "*_*_*.json"))):
         d = json.loads(open(f).read().strip().splitlines()[-1])
     except Exception:
         continue
-    rows.setdefault((m.group(2), m.group(1)), []).append(d.get("kernel_ms"))
+    v = d.get("kernel_ms") or (d.get("roofline") or {}).get("kernel_ms") or d.get("stamp_wbuf_us")
+    rows.setdefault((m.group(2), m.group(1)), []).append(v)
 for (w, v), ks in sorted(rows.items()):
     print(f"{w:10s} {v:8s} " + " ".join(f"{k:.3f}" for k in ks))
