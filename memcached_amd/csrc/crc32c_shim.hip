@@ -365,7 +365,13 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st, 
     // groups 190 us); k_count: 4096 (1024 measured 25 % slower on config 3).
     const int gf = (int)std::min<uint64_t>((n + 255) / 256, 1024);
     if (!counted && takes_small<MODE>(a)) {
-        hipLaunchKernelGGL((mcrc_dev::k_small<MODE>), dim3((unsigned)((n + 31) / 32)), dim3(1024),
+        // spans per workgroup: enough workgroups to reach every CU (one fits a
+        // CU: 160 KiB of tables), at least 8 so that each workgroup's table
+        // copy stays a few round trips; MCRC_SMALL_SPANS overrides (dev A/B)
+        const char *e = getenv("MCRC_SMALL_SPANS");
+        uint64_t per = e ? strtoull(e, nullptr, 10) : (n + d.cus - 1) / std::max(d.cus, 1);
+        per = std::min<uint64_t>(32, std::max<uint64_t>(e ? 2 : 8, (per + 1) & ~1ull));
+        hipLaunchKernelGGL((mcrc_dev::k_small<MODE>), dim3((unsigned)((n + per - 1) / per)), dim3((unsigned)(32 * per)),
                            mcrc_dev::kLdsImageK1Bytes, st, a, d.img);
         HIP_OK(hipGetLastError());
         return CRC32C_OK;
