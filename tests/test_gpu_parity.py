@@ -500,6 +500,26 @@ def test_config3_full_size(torch, span_path):
     bench._KEEP.clear()
 
 
+@pytest.mark.parametrize("wbuf", [61, 64, 100, 127, 4099])
+def test_verify_pages_tiny_wbufs(torch, wbuf):
+    """wbufs barely larger than one image (one item each, 48-B tail rule at
+    the edge), a buffer that ends inside a wbuf, and buffers shorter than a
+    header: the device walk and verify give the sequential walk's items."""
+    rng = np.random.default_rng(wbuf)
+    items = [layout.make_item(b"k", rng.integers(0, 256, int(rng.integers(0, 3)), dtype=np.uint8).tobytes(),
+                              cas=i + 1) for i in range(3000)]
+    items = [it for it in items if len(it) <= wbuf]
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    ok, nbad = mc.stamp_items(buf, offs, region_bytes=wbuf)
+    assert nbad == 0
+    for cut in (0, wbuf // 2, buf.size - 47, buf.size - 1):
+        b = buf[:buf.size - cut] if cut < buf.size else buf[:1]
+        want = _walk(b, wbuf)
+        got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, b), wbuf)
+        np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), want)
+        assert nbad == int((got_ok.cpu().numpy() == 0).sum())
+
+
 def test_chained_iovs(torch):
     """Chunked items (storage.c:163-170): the CRC chained over an item's iovs
     (header from +32, then each chunk) equals crc32c(0, concatenation)."""
