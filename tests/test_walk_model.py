@@ -108,3 +108,19 @@ def test_round_trips():
     buf = _pages(rng, [4096] * 1007, wbuf)
     got, trips = wave_walk(buf, 0, wbuf)
     assert len(got) == 1007 and trips == 1 + -(-1006 // WAVE) + (1 if 1006 % WAVE == 0 else 0)
+
+
+@pytest.mark.parametrize("wbuf", [48, 49, 61, 64, 100, 127])
+def test_tiny_wbufs(wbuf):
+    """wbufs that hold at most one image, and buffers cut inside a wbuf or
+    shorter than a header."""
+    rng = np.random.default_rng(wbuf)
+    items = [layout.make_item(b"k", rng.integers(0, 256, int(rng.integers(0, 3)), dtype=np.uint8).tobytes(),
+                              cas=i + 1) for i in range(200)]
+    items = [it for it in items if len(it) <= wbuf]
+    if items:
+        buf, _ = layout.pack_wbufs(items, wbuf)
+    else:
+        buf = np.zeros(3 * wbuf, np.uint8)
+    for cut in (0, wbuf // 2, max(buf.size - 47, 0)):
+        _check(buf[:buf.size - cut], wbuf)
