@@ -508,6 +508,10 @@ struct SpanArgs {
     uint32_t *span_acc;        // planned batches: R per span (segment units XOR their shifted values in)
     const uint32_t *segpow;    // rows k (x^i * x^(8 * 64Ki * k), i < 32) for k < 256, then k = 256 j
     uint64_t region;           // MODE 1: items never cross a multiple of `region` (0: no bound)
+    // k_small only (nullptr: nbad is the caller's to zero and read): the last
+    // workgroup moves *nbad to this pinned host word and zeroes *nbad and *done
+    unsigned long long *host_nbad;
+    uint32_t *done;            // finished workgroups
 };
 
 struct ItemDesc {
@@ -1411,6 +1415,21 @@ __global__ __launch_bounds__(1024) void k_small(SpanArgs a, const uint4 *__restr
     // so no workgroup-level sum as in count_bad)
     const uint64_t m = __ballot(nb != 0);
     if (m && lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) atomicAdd(a.nbad, (unsigned long long)__popcll(m));
+    if (a.host_nbad) {
+        // the last workgroup to finish hands the count to the host and leaves
+        // the counters at zero for the next call: no memset before the launch
+        // and no copy after it (two dispatches of a ~35 us synchronous call)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(a.done, 1u) == gridDim.x - 1) {
+                __threadfence();
+                *a.host_nbad = atomicExch(a.nbad, 0ull);
+                atomicExch(a.done, 0u);
+                __threadfence_system();
+            }
+        }
+    }
 }
 
 // ===========================================================================

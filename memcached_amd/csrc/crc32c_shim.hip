@@ -73,6 +73,10 @@ struct Device {
     uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
     unsigned long long *nbad = nullptr;
     unsigned long long *hbad = nullptr;  // pinned twin of nbad (a D2H copy into pageable memory is a slow path)
+    // k_small's own counters for calls that take the count from hbad (item
+    // images): zero between calls, kept so by the kernel's last workgroup
+    unsigned long long *small_nbad = nullptr;
+    uint32_t *small_done = nullptr;
     hipStream_t stream = nullptr, copy = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};  // host-batch pipeline slots
@@ -210,6 +214,9 @@ int init_device(Device &d, int id) {
     HIP_OK(hipMemset(d.zero, 0, mcrc_dev::kZeroBytes));
     HIP_OK(hipMalloc(&d.nbad, sizeof(unsigned long long)));
     HIP_OK(hipHostMalloc(&d.hbad, sizeof(unsigned long long), hipHostMallocDefault));
+    HIP_OK(hipMalloc(&d.small_nbad, 16));
+    HIP_OK(hipMemset(d.small_nbad, 0, 16));
+    d.small_done = reinterpret_cast<uint32_t *>(d.small_nbad + 1);
     HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&d.ev0));
@@ -347,7 +354,8 @@ uint64_t plan_cap(const mcrc_dev::SpanArgs &a) {
 // counted: the plan entries of k_count (unit counts, item records, one-block
 // flags, zeroed accumulators) are already written (the page walk's second pass).
 template <int MODE>
-int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st, bool counted = false) {
+int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st, bool counted = false,
+                 bool *host_counted = nullptr) {
     const uint64_t n = a.n;
     const bool identity = MODE == 0 && a.lens == nullptr && a.len <= mcrc_dev::kSegBytes;
     (void)aligned;
@@ -365,6 +373,12 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st, 
     // groups 190 us); k_count: 4096 (1024 measured 25 % slower on config 3).
     const int gf = (int)std::min<uint64_t>((n + 255) / 256, 1024);
     if (!counted && takes_small<MODE>(a)) {
+        if (host_counted) {  // the count arrives in d.hbad (k_small's last workgroup)
+            a.nbad = d.small_nbad;
+            a.host_nbad = d.hbad;
+            a.done = d.small_done;
+            *host_counted = true;
+        }
         // spans per workgroup: enough workgroups to reach every CU (one fits a
         // CU: 160 KiB of tables), at least 8 so that each workgroup's table
         // copy stays a few round trips; MCRC_SMALL_SPANS overrides (dev A/B)
@@ -711,8 +725,10 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
     a.zero = d->zero;
     a.region = region_bytes;
     d->acquire(st);
-    (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
-    rc = launch_units<MODE>(*d, a, false, st);
+    const bool small = takes_small<MODE>(a);  // (then the count comes back in d->hbad)
+    if (!small) (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
+    bool host_counted = false;
+    rc = launch_units<MODE>(*d, a, false, st, false, &host_counted);
     d->release(st);
     if (rc) {
         cleanup();
@@ -722,7 +738,7 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
     unsigned long long bad = 0;
     std::vector<uint32_t> crcs;
     std::vector<uint8_t> oks;
-    bool fail = hipMemcpyAsync(d->hbad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st) != hipSuccess;
+    bool fail = !host_counted && hipMemcpyAsync(d->hbad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st) != hipSuccess;
     if (!dev && MODE == 1) fail = fail || hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, st) != hipSuccess;
     if (!dev && MODE == 2) {
         crcs.resize(n);
