@@ -591,11 +591,16 @@ def extra_workload(args):
         hout = np.empty(64, np.uint32)
         hs = _lib.Spans(host.ctypes.data, host.size, hoffs.ctypes.data, 0, None, 4133, None, hout.ctypes.data, 64)
         host64_us = per_call(lambda: _lib.check(_lib.lib.crc32c_batch(ctypes.byref(hs), 0, None)), 200)
+        # 64 device spans by offsets (the read-back IO batch as raw spans)
+        doffs64 = (torch.arange(64, device="cuda", dtype=torch.int64) * 4165 + 32).contiguous()
+        dout64 = torch.empty(64, dtype=torch.int32, device="cuda")
+        ds = _lib.Spans(base, region, doffs64.data_ptr(), 0, None, 4133, None, dout64.data_ptr(), 64)
+        dev64_us = per_call(lambda: _lib.check(_lib.lib.crc32c_batch(ctypes.byref(ds), _lib.CRC32C_DEVICE, sptr)), 200)
         res.update(config={"workload": "per-call latency, synchronous calls: stamp one 4 MiB wbuf of 1007 images "
                                        "(device), verify an IO batch of 64 images (device), CRC 64 x 4133-B "
-                                       "spans in pageable host memory (host path)"},
+                                       "spans in pageable host memory (host path) and in device memory"},
                    stamp_wbuf_us=round(stamp_us, 1), verify64_us=round(verify64_us, 1),
-                   host_batch64_us=round(host64_us, 1),
+                   host_batch64_us=round(host64_us, 1), device_batch64_us=round(dev64_us, 1),
                    stamp_wbuf_gb_s=round(per_wbuf * 4133 / (stamp_us * 1e-6) / 1e9, 1))
     else:  # host: pinned host memory -> H2D -> K1/K2 -> D2H through the library's host path
         import numpy as np

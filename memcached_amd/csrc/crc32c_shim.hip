@@ -457,7 +457,9 @@ bool fixed_spans_fit(const crc32c_spans &s) {
     return (s.n - 1) <= (s.base_bytes - s.len) / s.stride;
 }
 
-int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t st) {
+// host_counted (synchronous callers only): a small batch's out-of-range count
+// comes back in d.hbad from k_small itself (no memset, no copy).
+int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t st, bool *host_counted = nullptr) {
     if (s.n == 0) return CRC32C_OK;
     if (!fixed_spans_fit(s)) return CRC32C_EINVAL;
     const bool fixed = s.offsets == nullptr && s.lens == nullptr;
@@ -490,10 +492,11 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
     a.xpow = d.xpow;
     a.tab8 = d.tab8;
     a.zero = d.zero;
-    HIP_OK(hipMemsetAsync(d.nbad, 0, sizeof(unsigned long long), st));
+    const bool small = host_counted && takes_small<0>(a);
+    if (!small) HIP_OK(hipMemsetAsync(d.nbad, 0, sizeof(unsigned long long), st));
     const bool aligned = (flags & CRC32C_ALIGNED16) ||
                          (fixed && aligned16(s.base) && (s.stride & 15u) == 0 && (s.len & 15u) == 0);
-    return launch_units<0>(d, a, aligned, st);
+    return launch_units<0>(d, a, aligned, st, false, small ? host_counted : nullptr);
 }
 
 // [p, p + bytes) lies inside one device allocation (so no kernel read bounded
@@ -816,7 +819,8 @@ int crc32c_batch(const crc32c_spans *s, unsigned flags, void *stream) {
     std::lock_guard<std::mutex> lk(d->mu);
     d->acquire(st);
     if (timed) HIP_OK(hipEventRecord(d->ev0, st));
-    rc = enqueue_device(*d, *s, flags, st);
+    bool host_counted = false;
+    rc = enqueue_device(*d, *s, flags, st, timed ? &host_counted : nullptr);
     if (rc) {
         d->release(st);
         return rc;
@@ -829,7 +833,7 @@ int crc32c_batch(const crc32c_spans *s, unsigned flags, void *stream) {
     // spans given by offsets / lengths are range-checked on the device
     unsigned long long nrange = 0;
     const bool checked = s->n && (s->offsets || s->lens);
-    if (checked) HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
+    if (checked && !host_counted) HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
     d->release(st);
     HIP_OK(hipEventSynchronize(d->ev1));
     if (checked) {
