@@ -157,34 +157,20 @@ def settle(step, ms: float) -> int:
     return n
 
 
-def cpu_baseline(data: torch.Tensor, out: torch.Tensor):
-    """Reference crc32c.c on host cores over a bounded sample of the batch."""
-    ref = os.path.join(ROOT, "oracle", "_ref", "libref_crc32c.so")
-    if not os.path.exists(ref):
-        return {"value": None, "unit": "GiB/s", "cores": 0, "kind": "reference",
-                "sample": "oracle/_ref/libref_crc32c.so missing (build in the container with /root/reference)"}
-    lib = ctypes.CDLL(ref)
-    lib.ref_crc32c_init()
-    lib.ref_crc32c_batch_timed.restype = ctypes.c_double
-    lib.ref_crc32c_batch_timed.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
-                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
-    n = 1 << 16  # 256 MiB sample: the first 65536 items of rank 0's batch
-    host = data[: n * ITEM_BYTES].cpu().numpy()
-    import numpy as np
-    crc = np.empty(n, np.uint32)
-    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-
-    def rate(threads, passes):
-        best = 0.0
-        lib.ref_crc32c_batch_timed(host.ctypes.data, None, None, ITEM_BYTES, ITEM_BYTES, n, threads, crc.ctypes.data)
-        for _ in range(passes):
-            t = lib.ref_crc32c_batch_timed(host.ctypes.data, None, None, ITEM_BYTES, ITEM_BYTES, n, threads,
-                                           crc.ctypes.data)
-            best = max(best, n * ITEM_BYTES / t / 2**30)
-        return best
-
-    one = rate(1, 5)
-    many = rate(cores, 20)
+def cpu_topology():
+    """Physical cores among the CPUs this process may run on: one logical CPU
+    per (package, core) pair, from /sys topology.  Returns (cpus, sockets,
+    logical count, model name)."""
+    logical = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
+    first, pkgs = {}, set()
+    for c in logical:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            key = (int(open(base + "physical_package_id").read()), int(open(base + "core_id").read()))
+        except (OSError, ValueError):
+            key = (0, c)
+        pkgs.add(key[0])
+        first.setdefault(key, c)
     model = "unknown CPU"
     try:
         for line in open("/proc/cpuinfo"):
@@ -193,12 +179,55 @@ def cpu_baseline(data: torch.Tensor, out: torch.Tensor):
                 break
     except OSError:
         pass
+    return sorted(first.values()), len(pkgs), len(logical), model
+
+
+def cpu_baseline(data: torch.Tensor, out: torch.Tensor):
+    """Reference crc32c.c on the host cores over the whole batch: one pthread
+    per physical core (pinned, static contiguous split, best of 10 after a
+    warm-up pass), plus the 1-core and 16-thread figures (16 = one GPU's share
+    of the box's CPUs)."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "libref_crc32c.so")
+    if not os.path.exists(ref):
+        return {"value": None, "unit": "GiB/s", "cores": 0, "kind": "reference",
+                "sample": "oracle/_ref/libref_crc32c.so missing (build in the container with /root/reference)"}
+    import numpy as np
+    lib = ctypes.CDLL(ref)
+    lib.ref_crc32c_init()
+    lib.ref_crc32c_batch_timed_cpus.restype = ctypes.c_double
+    lib.ref_crc32c_batch_timed_cpus.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
+                                                ctypes.c_void_p]
+    n = out.numel()
+    host = data[: n * ITEM_BYTES].cpu().numpy()
+    crc = np.empty(n, np.uint32)
+    cpus, sockets, nlogical, model = cpu_topology()
+    cores = len(cpus)
+    cpu_arr = np.asarray(cpus, np.int32)
+
+    def rate(threads, passes, items):
+        best = 0.0
+        pin = cpu_arr.ctypes.data if threads <= cores else None
+        lib.ref_crc32c_batch_timed_cpus(host.ctypes.data, None, None, ITEM_BYTES, ITEM_BYTES, items, threads,
+                                        crc.ctypes.data, pin)
+        for _ in range(passes):
+            t = lib.ref_crc32c_batch_timed_cpus(host.ctypes.data, None, None, ITEM_BYTES, ITEM_BYTES, items, threads,
+                                                crc.ctypes.data, pin)
+            best = max(best, items * ITEM_BYTES / t / 2**30)
+        return best
+
+    one = rate(1, 3, min(n, 1 << 16))   # 1 core: the first 256 MiB, best of 3
+    sixteen = rate(min(16, cores), 5, n)
+    many = rate(cores, 10, n)           # last: crc[] then holds every item's CRC
     gpu = out[:n].cpu().numpy().view(np.uint32)
     return {"value": round(many, 2), "unit": "GiB/s", "cores": cores, "kind": "reference",
-            "sample": f"first 65536 x 4096 B items of the GPU batch (256 MiB), reference crc32c.c "
-                      f"(hw dispatch) per item as storage.c:567, {cores} threads static split, best of 20; "
-                      f"1 core: {one:.2f} GiB/s; {model}",
-            "gpu_match": bool((gpu == crc).all())}
+            "sample": f"the whole GPU batch ({n} x {ITEM_BYTES} B, {n * ITEM_BYTES / 2**30:.0f} GiB) in host memory, "
+                      f"reference crc32c.c (hw dispatch) per item as storage.c:567, one pinned pthread per physical "
+                      f"core ({cores} cores, {sockets} socket(s), {nlogical} logical CPUs), static contiguous split, "
+                      f"best of 10; 16 threads: {sixteen:.2f} GiB/s; 1 core: {one:.2f} GiB/s (first 65536 items); "
+                      f"{model}",
+            "one_core": round(one, 2), "sixteen_threads": round(sixteen, 2), "sockets": sockets,
+            "cpu_model": model, "gpu_match": bool((gpu == crc).all())}
 
 
 def zipf_lens(n: int, seed: int = 7):
@@ -377,17 +406,18 @@ def workload_pagesmix(args, rank, world):
         "items_le_4k_frac": round(float((ntot_np <= 4096).mean()), 3), "injected_bad": int(victims.numel())}
 
 
-def traffic_per_launch():
-    """HBM bytes per K1 launch from the committed rocprofv3 --pmc summary, if any."""
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
-    if not paths:
-        return None
-    try:
-        rec = json.load(open(paths[-1]))
-        if rec.get("items") == ITEMS_PER_GPU and rec.get("item_bytes") == ITEM_BYTES:
-            return rec.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+def traffic_per_launch(items=ITEMS_PER_GPU, item_bytes=ITEM_BYTES):
+    """HBM bytes per K1 launch from the committed rocprofv3 --pmc summaries:
+    the newest profiles/*traffic*.json record of kernel k_fixed measured on
+    this batch shape (files of other kernels or shapes are skipped)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
+        try:
+            rec = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if (isinstance(rec, dict) and rec.get("kernel") == "k_fixed" and rec.get("items") == items
+                and rec.get("item_bytes") == item_bytes and rec.get("hbm_bytes_per_launch")):
+            return rec["hbm_bytes_per_launch"]
     return None
 
 
@@ -408,7 +438,8 @@ def main():
     ap.add_argument("--fill", default="splitmix", choices=["splitmix", "randint"],
                     help="item bytes: splitmix64(42 + rank) words (SURVEY.md 8d) or torch.randint")
     ap.add_argument("--workload", default="config2",
-                    choices=["config2", "config2r", "config3", "config5", "pagesmix", "pages", "stamp", "host", "calls"],
+                    choices=["config2", "config2r", "config3", "config5", "pagesmix", "pages", "stamp", "host", "calls",
+                             "multi"],
                     help="config2 = headline; others are extra measurements (not the bench line)")
     ap.add_argument("--pages", type=int, default=1000, help="config5: 64 MiB pages per GPU")
     ap.add_argument("--span-len", type=int, default=4133, help="config2r: span length (stride = len + 32)")
@@ -480,8 +511,92 @@ def main():
         dist.destroy_process_group()
 
 
+def workload_multi(args):
+    """BASELINE configs[3] in one process: 1 Mi x 4 KiB items per GPU on the
+    first --gpus devices (no collective; a shard per device).
+
+    device: each device's shard resident in its HBM, K1 launched on every
+            device (one stream each), all enqueued before any is waited for;
+            value = all devices' bytes / wall time of the K steps.
+    host:   the same bytes in one pinned host buffer, split by
+            crc32c_batch_multi (crc32c_shard_cuts, one host thread per device,
+            pinned H2D / kernel / D2H overlapped in two pipeline slots):
+            the PCIe-inclusive rate.
+    Both modes' CRCs must agree item for item."""
+    import numpy as np
+    ng = args.gpus
+    if torch.cuda.device_count() < ng:
+        raise SystemExit(f"--gpus {ng} but {torch.cuda.device_count()} visible devices")
+    n = args.items
+    flags = _lib.CRC32C_DEVICE | _lib.CRC32C_ASYNC
+    dev = []
+    for g in range(ng):
+        torch.cuda.set_device(g)
+        data = splitmix64_bytes(n * ITEM_BYTES, 42 + g, device=f"cuda:{g}")
+        out = torch.empty(n, dtype=torch.int32, device=f"cuda:{g}")
+        sp = _lib.Spans(data.data_ptr(), data.numel(), None, ITEM_BYTES, None, ITEM_BYTES, None, out.data_ptr(), n)
+        dev.append((g, data, out, sp, torch.cuda.Stream(device=g)))
+
+    def launch(k, evs=None):
+        for i in range(k):
+            for g, data, out, sp, st in dev:
+                torch.cuda.set_device(g)
+                if evs is not None and i == 0:
+                    evs[g][0].record(st)
+                _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp), flags, ctypes.c_void_p(st.cuda_stream)))
+                if evs is not None and i == k - 1:
+                    evs[g][1].record(st)
+
+    def sync_all():
+        for g, *_ in dev:
+            torch.cuda.synchronize(g)
+
+    settled = settle(lambda k: (launch(k), sync_all()), args.settle_ms)
+    launch(max(1, args.warmup))
+    sync_all()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(ng)]
+    t0 = time.perf_counter()
+    launch(args.steps, evs)
+    sync_all()
+    el = time.perf_counter() - t0
+    kms = [evs[g][0].elapsed_time(evs[g][1]) / args.steps for g in range(ng)]
+    nbytes = ng * n * ITEM_BYTES
+    res = {"device": {"gib_s": round(nbytes * args.steps / el / 2**30, 2), "ms_per_step": round(el / args.steps * 1e3, 4),
+                      "kernel_ms_per_device": [round(x, 4) for x in kms],
+                      "hbm_frac_per_device": [round(n * ITEM_BYTES / (x * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for x in kms],
+                      "settle_launches": settled}}
+    # host-resident: the same bytes in one pinned buffer
+    host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    for g, data, *_ in dev:
+        host[g * n * ITEM_BYTES:(g + 1) * n * ITEM_BYTES].copy_(data)
+    hout = np.empty(ng * n, np.uint32)
+    hs = _lib.Spans(host.data_ptr(), nbytes, None, ITEM_BYTES, None, ITEM_BYTES, None, hout.ctypes.data, ng * n)
+    _lib.check(_lib.lib.crc32c_batch_multi(ctypes.byref(hs), ng))  # warm-up (pipeline buffers)
+    hsteps = max(1, min(args.steps, 5))
+    t0 = time.perf_counter()
+    for _ in range(hsteps):
+        _lib.check(_lib.lib.crc32c_batch_multi(ctypes.byref(hs), ng))
+    el = time.perf_counter() - t0
+    res["host"] = {"gib_s": round(nbytes * hsteps / el / 2**30, 2), "gb_s": round(nbytes * hsteps / el / 1e9, 2),
+                   "ms_per_step": round(el / hsteps * 1e3, 2), "steps": hsteps}
+    want = np.concatenate([out.cpu().numpy().view(np.uint32) for _, _, out, _, _ in dev])
+    res["crc_match"] = bool((want == hout).all())
+    cuts = np.empty(ng + 1, np.uint64)
+    _lib.check(_lib.lib.crc32c_shard_cuts(None, ITEM_BYTES, ng * n, ng, cuts.ctypes.data))
+    res["config"] = {"workload": f"BASELINE configs[3] shape: {n} x {ITEM_BYTES} B items per GPU on {ng} GPU(s), "
+                                 "one process; device-resident K1 on every device, and the same bytes in pinned host "
+                                 "memory through crc32c_batch_multi (PCIe-inclusive)",
+                     "items_per_gpu": n, "shard_cuts": [int(c) for c in cuts]}
+    return res
+
+
 def extra_workload(args):
     """Non-headline measurements; prints one JSON line per run."""
+    if args.workload == "multi":  # one process drives every device (no torchrun)
+        res = {"workload_kind": "multi", "n_gpus": args.gpus, "steps": args.steps}
+        res.update(workload_multi(args))
+        print(json.dumps(res), flush=True)
+        return
     rank, world, local = dist_setup(args.gpus)
     stream = torch.cuda.current_stream()
     res = {"workload_kind": args.workload, "n_gpus": world, "steps": args.steps}
@@ -596,12 +711,35 @@ def extra_workload(args):
         dout64 = torch.empty(64, dtype=torch.int32, device="cuda")
         ds = _lib.Spans(base, region, doffs64.data_ptr(), 0, None, 4133, None, dout64.data_ptr(), 64)
         dev64_us = per_call(lambda: _lib.check(_lib.lib.crc32c_batch(ctypes.byref(ds), _lib.CRC32C_DEVICE, sptr)), 200)
-        res.update(config={"workload": "per-call latency, synchronous calls: stamp one 4 MiB wbuf of 1007 images "
-                                       "(device), verify an IO batch of 64 images (device), CRC 64 x 4133-B "
-                                       "spans in pageable host memory (host path) and in device memory"},
+        # host-resident item calls: one wbuf in page-locked
+        # memory (crc32c_host_alloc / pin_memory) and in pageable memory
+        wb_dev = _KEEP[-2][:region]  # (the config-5 page tensor; its first wbuf)
+        wb_pin = wb_dev.cpu().pin_memory()
+        wb_page = wb_dev.cpu().numpy().copy()
+        hoffs_w = (np.arange(per_wbuf, dtype=np.uint64) * 4165).astype(np.uint64)
+        hok = np.empty(per_wbuf, np.uint8)
+        stamp_pin_us = per_call(lambda: _lib.check(_lib.lib.crc32c_stamp_items(
+            wb_pin.data_ptr(), region, region, hoffs_w.ctypes.data, per_wbuf, None, ctypes.byref(nbad), 0, None)), 100)
+        stamp_page_us = per_call(lambda: _lib.check(_lib.lib.crc32c_stamp_items(
+            wb_page.ctypes.data, region, region, hoffs_w.ctypes.data, per_wbuf, None, ctypes.byref(nbad), 0, None)), 50)
+        verify64_pin_us = per_call(lambda: _lib.check(_lib.lib.crc32c_verify_items(
+            wb_pin.data_ptr(), region, region, hoffs_w.ctypes.data, 64, hok.ctypes.data, ctypes.byref(nbad), 0,
+            None)), 200)
+        pin64 = torch.from_numpy(host).pin_memory()
+        hs_pin = _lib.Spans(pin64.data_ptr(), host.size, hoffs.ctypes.data, 0, None, 4133, None, hout.ctypes.data, 64)
+        host64_pin_us = per_call(lambda: _lib.check(_lib.lib.crc32c_batch(ctypes.byref(hs_pin), 0, None)), 200)
+        res.update(config={"workload": "per-call latency, synchronous calls, one thread: stamp one 4 MiB wbuf of "
+                                       "1007 images (device; host page-locked; host pageable), verify an IO batch "
+                                       "of 64 images (device; host page-locked), CRC 64 x 4133-B spans in host "
+                                       "memory (pageable: staged; page-locked: the coalescing queue) and in device "
+                                       "memory"},
                    stamp_wbuf_us=round(stamp_us, 1), verify64_us=round(verify64_us, 1),
-                   host_batch64_us=round(host64_us, 1), device_batch64_us=round(dev64_us, 1),
-                   stamp_wbuf_gb_s=round(per_wbuf * 4133 / (stamp_us * 1e-6) / 1e9, 1))
+                   stamp_wbuf_host_pinned_us=round(stamp_pin_us, 1), stamp_wbuf_host_pageable_us=round(stamp_page_us, 1),
+                   verify64_host_pinned_us=round(verify64_pin_us, 1),
+                   host_batch64_us=round(host64_us, 1), host_batch64_pinned_us=round(host64_pin_us, 1),
+                   device_batch64_us=round(dev64_us, 1),
+                   stamp_wbuf_gb_s=round(per_wbuf * 4133 / (stamp_us * 1e-6) / 1e9, 1),
+                   stamp_wbuf_host_pinned_gb_s=round(per_wbuf * 4133 / (stamp_pin_us * 1e-6) / 1e9, 1))
     else:  # host: pinned host memory -> H2D -> K1/K2 -> D2H through the library's host path
         import numpy as np
         n = args.items

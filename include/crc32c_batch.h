@@ -23,7 +23,11 @@
  *                          rank 3).
  *   crc32c_batch_multi     crc32c_batch for host-resident batches split across
  *                          several GPUs by bytes (no collective: items are
- *                          independent).
+ *                          independent); crc32c_shard_cuts is its split.
+ *   crc32c_batch_submit    the read-verify CRCs of many IO threads
+ *   / crc32c_batch_wait    (extstore.c:853-945, one batch of <= io_depth reads
+ *                          per thread) coalesced into one kernel launch per
+ *                          dispatch by a per-device queue.
  *
  * Results are bit-identical to the reference crc32c.c.  There is no CPU
  * fallback: without a usable gfx950 device every batch entry point returns
@@ -54,6 +58,10 @@ extern "C" {
 #define CRC32C_ASYNC 0x2u     /* with CRC32C_DEVICE: enqueue on `stream`, do not wait */
 #define CRC32C_ALIGNED16 0x4u /* caller guarantees every span start and length is a
                                  multiple of 16 bytes (selects the aligned kernel) */
+#define CRC32C_CFLAGS64 0x8u  /* item-image calls: the images come from a build with
+                                 --enable-large-client-flags (configure.ac:139-140):
+                                 client_flags_t is 8 bytes, so ITEM_CFLAGS adds 8 to
+                                 ITEM_ntotal instead of 4 (memcached.h:96-100, :149-152) */
 
 /* A batch of byte spans inside one buffer.
  *   span i = [base + (offsets ? offsets[i] : i * stride),  + (lens ? lens[i] : len))
@@ -90,6 +98,13 @@ int crc32c_batch(const crc32c_spans *spans, unsigned flags, void *stream);
 /* Host batch split across the first `ngpus` devices by bytes; one host thread
  * per device, pinned H2D / D2H overlapped with the kernels. */
 int crc32c_batch_multi(const crc32c_spans *spans, int ngpus);
+
+/* The split crc32c_batch_multi uses: parts + 1 cut points, part g owns spans
+ * [cuts[g], cuts[g+1]).  cuts[g] is the first span index i whose byte prefix
+ * sum(len[0..i)) reaches total * g / parts (total = every span's bytes), so
+ * each part holds about total / parts bytes.  lens == NULL: every span is
+ * `len` bytes.  (The Python twin is memcached_amd/shard.py plan().) */
+int crc32c_shard_cuts(const uint32_t *lens, uint32_t len, uint64_t n, int parts, uint64_t *cuts);
 
 /* Verify n item images of a packed page buffer (host or device per flags).
  * ok[i] = 1 when item i's CRC matches its stored exptime; *nbad receives the
@@ -138,11 +153,28 @@ int crc32c_stamp_items(void *base, uint64_t base_bytes, uint64_t region_bytes,
                        const uint64_t *item_offsets, uint64_t n, uint8_t *ok, uint64_t *nbad,
                        unsigned flags, void *stream);
 
-/* Asynchronous form of crc32c_batch for host batches: returns at once with a
- * job handle; crc32c_batch_wait blocks until out[] is filled and frees it. */
+/* Asynchronous form of crc32c_batch: returns at once with a job handle;
+ * crc32c_batch_wait blocks until out[] is filled and frees the handle.
+ *
+ * Jobs go to the current device's queue.  Host jobs whose buffer is
+ * device-visible (crc32c_host_alloc, crc32c_host_register) and whose spans are
+ * at most 256 KiB are coalesced: the queue's dispatcher packs every such job
+ * pending at that moment (up to 8192 spans) into one kernel launch that reads
+ * the spans straight from host memory, while the previous launch runs.  Many
+ * IO threads that each submit their few reads (storage.c:172 per io_depth
+ * batch) thus share launches; crc32c_batch itself takes this path for such
+ * batches.  Other jobs (pageable host memory, long spans, CRC32C_DEVICE
+ * batches, which must be complete in device memory when submitted) run one
+ * by one on the dispatcher.  The caller's arrays must stay valid until
+ * crc32c_batch_wait returns. */
 typedef struct crc32c_job *crc32c_job_t;
 int crc32c_batch_submit(const crc32c_spans *spans, unsigned flags, crc32c_job_t *job);
 int crc32c_batch_wait(crc32c_job_t job);
+
+/* Queue counters of the current device since the first submit: coalesced
+ * kernel launches, the spans and jobs they carried, and jobs run alone.  Any
+ * pointer may be NULL. */
+int crc32c_queue_stats(uint64_t *launches, uint64_t *spans, uint64_t *jobs, uint64_t *solo_jobs);
 
 /* Page-locked host memory for extstore's wbufs (extstore.c:127-140) and the
  * compaction readback_buf (storage.c:1120): host batches over such buffers
@@ -151,6 +183,18 @@ int crc32c_batch_wait(crc32c_job_t job);
  * crc32c_host_free. */
 void *crc32c_host_alloc(size_t bytes);
 void crc32c_host_free(void *p);
+
+/* Page-lock and map an existing host range (e.g. the slab arena that read
+ * buffers come from, storage.c:264-337) so host batches over it are read by
+ * the GPU in place: coalesced by the queue and copied without staging. */
+int crc32c_host_register(void *p, size_t bytes);
+int crc32c_host_unregister(void *p);
+
+/* Tuning, for tests and benchmarks: batches of at most n spans (default 8192,
+ * the kernel's limit) take the single-launch small-batch kernel; 0 sends every
+ * batch through the planned multi-launch path.  Process-wide; returns the
+ * previous value. */
+uint64_t crc32c_set_small_max(uint64_t n);
 
 const char *crc32c_strerror(int err);
 

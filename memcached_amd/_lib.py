@@ -11,7 +11,7 @@ import ctypes
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-# MCRC_LIB selects another build of the same library (ablation builds, tools/ablate_spans.sh)
+# MCRC_LIB selects another build of the same library (A/B of two builds in one run)
 LIB_PATH = os.environ.get("MCRC_LIB") or os.path.join(PKG, "libmcrc32c.so")
 
 CRC32C_OK = 0
@@ -24,6 +24,7 @@ CRC32C_ERANGE = -5
 CRC32C_DEVICE = 0x1
 CRC32C_ASYNC = 0x2
 CRC32C_ALIGNED16 = 0x4
+CRC32C_CFLAGS64 = 0x8
 
 # every symbol include/*.h declares (checked by tests/test_abi.py)
 EXPORTED = (
@@ -31,6 +32,8 @@ EXPORTED = (
     "crc32c_gpu_count", "crc32c_batch", "crc32c_batch_multi", "crc32c_verify_items", "crc32c_stamp_items",
     "crc32c_verify_pages", "crc32c_batch_chains", "crc32c_host_alloc", "crc32c_host_free",
     "crc32c_batch_submit", "crc32c_batch_wait", "crc32c_strerror", "crc32c_last_kernel_ms",
+    "crc32c_shard_cuts", "crc32c_queue_stats", "crc32c_host_register", "crc32c_host_unregister",
+    "crc32c_set_small_max",
 )
 
 
@@ -98,6 +101,17 @@ def _load():
     lib.crc32c_strerror.restype = ctypes.c_char_p
     lib.crc32c_strerror.argtypes = [ctypes.c_int]
     lib.crc32c_last_kernel_ms.restype = ctypes.c_float
+    lib.crc32c_shard_cuts.restype = ctypes.c_int
+    lib.crc32c_shard_cuts.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int,
+                                      ctypes.c_void_p]
+    lib.crc32c_queue_stats.restype = ctypes.c_int
+    lib.crc32c_queue_stats.argtypes = [ctypes.POINTER(ctypes.c_uint64)] * 4
+    lib.crc32c_host_register.restype = ctypes.c_int
+    lib.crc32c_host_register.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    lib.crc32c_host_unregister.restype = ctypes.c_int
+    lib.crc32c_host_unregister.argtypes = [ctypes.c_void_p]
+    lib.crc32c_set_small_max.restype = ctypes.c_uint64
+    lib.crc32c_set_small_max.argtypes = [ctypes.c_uint64]
     lib.crc32c_init()
     return lib
 

@@ -22,10 +22,10 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import CRC32C_ALIGNED16, CRC32C_ASYNC, CRC32C_DEVICE, Crc32cError, check, lib
+from ._lib import CRC32C_ALIGNED16, CRC32C_ASYNC, CRC32C_CFLAGS64, CRC32C_DEVICE, Crc32cError, check, lib
 
-__all__ = ["crc32c", "crc32c_sw", "batch", "verify_items", "stamp_items", "verify_pages", "batch_chains", "batch_multi", "gpu_count",
-           "Crc32cError"]
+__all__ = ["crc32c", "crc32c_sw", "batch", "verify_items", "stamp_items", "verify_pages", "batch_chains", "batch_multi",
+           "shard_cuts", "queue_stats", "set_small_max", "gpu_count", "Crc32cError"]
 
 
 def _host_buf(data):
@@ -143,14 +143,16 @@ def batch_multi(buf, offsets=None, stride: int = 0, lens=None, length: int = 0, 
     return out
 
 
-def verify_items(buf, item_offsets, region_bytes=0, stream=None):
+def verify_items(buf, item_offsets, region_bytes=0, stream=None, cflags64=False):
     """Verify packed item images; returns (ok uint8 array / tensor, nbad).
 
     ``region_bytes``: the write-buffer size; an item whose header claims a
     span crossing a multiple of it is reported bad without being read
-    (extstore never splits an item across wbufs).  0 = no such bound."""
+    (extstore never splits an item across wbufs).  0 = no such bound.
+    ``cflags64``: images of a LARGE_CLIENT_FLAGS build (8-byte client flags)."""
     dev = _is_torch(buf) and buf.is_cuda
     nbad = ctypes.c_uint64(0)
+    fl = CRC32C_CFLAGS64 if cflags64 else 0
     if dev:
         import torch
         n = item_offsets.numel()
@@ -159,24 +161,25 @@ def verify_items(buf, item_offsets, region_bytes=0, stream=None):
         if stream is None:
             stream = torch.cuda.current_stream(buf.device).cuda_stream
         rc = lib.crc32c_verify_items(buf.data_ptr(), buf.numel() * buf.element_size(), region_bytes,
-                                     item_offsets.data_ptr(), n, ok.data_ptr(), ctypes.byref(nbad), CRC32C_DEVICE,
-                                     stream)
+                                     item_offsets.data_ptr(), n, ok.data_ptr(), ctypes.byref(nbad),
+                                     CRC32C_DEVICE | fl, stream)
     else:
         buf = _host_buf(buf)
         offs = np.ascontiguousarray(item_offsets, dtype=np.uint64)
         ok = np.empty(offs.size, dtype=np.uint8)
         rc = lib.crc32c_verify_items(buf.ctypes.data, buf.size, region_bytes, offs.ctypes.data, offs.size,
-                                     ok.ctypes.data, ctypes.byref(nbad), 0, None)
+                                     ok.ctypes.data, ctypes.byref(nbad), fl, None)
     check(rc, "crc32c_verify_items")
     return ok, int(nbad.value)
 
 
-def stamp_items(buf, item_offsets, region_bytes=0, stream=None):
+def stamp_items(buf, item_offsets, region_bytes=0, stream=None, cflags64=False):
     """Write the spill CRC of every item image into its exptime field, in place
     (storage.c:567 for a whole wbuf at once).  Returns (ok, nbad): ok marks
     stamped images, nbad counts malformed ones (left untouched)."""
     dev = _is_torch(buf) and buf.is_cuda
     nbad = ctypes.c_uint64(0)
+    fl = CRC32C_CFLAGS64 if cflags64 else 0
     if dev:
         import torch
         n = item_offsets.numel()
@@ -185,8 +188,8 @@ def stamp_items(buf, item_offsets, region_bytes=0, stream=None):
         if stream is None:
             stream = torch.cuda.current_stream(buf.device).cuda_stream
         rc = lib.crc32c_stamp_items(buf.data_ptr(), buf.numel() * buf.element_size(), region_bytes,
-                                    item_offsets.data_ptr(), n, ok.data_ptr(), ctypes.byref(nbad), CRC32C_DEVICE,
-                                    stream)
+                                    item_offsets.data_ptr(), n, ok.data_ptr(), ctypes.byref(nbad),
+                                    CRC32C_DEVICE | fl, stream)
     else:
         if not (isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and buf.flags.writeable
                 and buf.flags.c_contiguous):
@@ -194,12 +197,12 @@ def stamp_items(buf, item_offsets, region_bytes=0, stream=None):
         offs = np.ascontiguousarray(item_offsets, dtype=np.uint64)
         ok = np.empty(offs.size, dtype=np.uint8)
         rc = lib.crc32c_stamp_items(buf.ctypes.data, buf.size, region_bytes, offs.ctypes.data, offs.size,
-                                    ok.ctypes.data, ctypes.byref(nbad), 0, None)
+                                    ok.ctypes.data, ctypes.byref(nbad), fl, None)
     check(rc, "crc32c_stamp_items")
     return ok, int(nbad.value)
 
 
-def verify_pages(buf, wbuf_bytes, stream=None):
+def verify_pages(buf, wbuf_bytes, stream=None, cflags64=False):
     """Walk every wbuf-sized read of ``buf`` on the device and verify each
     item found.  Returns (item offsets, ok flags, nbad) in walk order.
 
@@ -208,6 +211,7 @@ def verify_pages(buf, wbuf_bytes, stream=None):
     count the first one reported."""
     dev = _is_torch(buf) and buf.is_cuda
     nitems, nbad = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    fl = CRC32C_CFLAGS64 if cflags64 else 0
     if dev:
         import torch
         if not buf.is_contiguous():
@@ -221,7 +225,7 @@ def verify_pages(buf, wbuf_bytes, stream=None):
             offs = torch.empty(cap, dtype=torch.int64, device=buf.device)
             ok = torch.empty(cap, dtype=torch.uint8, device=buf.device)
             check(lib.crc32c_verify_pages(buf.data_ptr(), nbytes, wbuf_bytes, offs.data_ptr(), ok.data_ptr(), cap,
-                                          ctypes.byref(nitems), ctypes.byref(nbad), CRC32C_DEVICE, stream),
+                                          ctypes.byref(nitems), ctypes.byref(nbad), CRC32C_DEVICE | fl, stream),
                   "crc32c_verify_pages")
             n = nitems.value
             if n <= cap:
@@ -233,7 +237,7 @@ def verify_pages(buf, wbuf_bytes, stream=None):
     offs = np.empty(cap, np.uint64)
     ok = np.empty(cap, np.uint8)
     check(lib.crc32c_verify_pages(buf.ctypes.data, buf.size, wbuf_bytes, offs.ctypes.data, ok.ctypes.data, cap,
-                                  ctypes.byref(nitems), ctypes.byref(nbad), 0, None), "crc32c_verify_pages")
+                                  ctypes.byref(nitems), ctypes.byref(nbad), fl, None), "crc32c_verify_pages")
     n = nitems.value
     assert n <= cap, "item count above the proven bound"
     return offs[:n], ok[:n], int(nbad.value)
@@ -269,3 +273,24 @@ def batch_chains(buf, offsets, lens, chain_first, stream=None):
     check(lib.crc32c_batch_chains(ctypes.byref(s), _ptr(chain_first), nchains, _ptr(out),
                                   CRC32C_DEVICE if dev else 0, stream if dev else None), "crc32c_batch_chains")
     return out
+
+
+def shard_cuts(lens, parts: int):
+    """crc32c_shard_cuts: the parts + 1 cut points of the byte-balanced split
+    crc32c_batch_multi uses over spans of lengths ``lens`` (uint32)."""
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    cuts = np.empty(parts + 1, dtype=np.uint64)
+    check(lib.crc32c_shard_cuts(lens.ctypes.data, 0, lens.size, parts, cuts.ctypes.data), "crc32c_shard_cuts")
+    return cuts.astype(np.int64)
+
+
+def queue_stats():
+    """(launches, spans, jobs, solo_jobs) of the current device's coalescing queue."""
+    v = [ctypes.c_uint64(0) for _ in range(4)]
+    check(lib.crc32c_queue_stats(*[ctypes.byref(x) for x in v]), "crc32c_queue_stats")
+    return tuple(int(x.value) for x in v)
+
+
+def set_small_max(n: int) -> int:
+    """Batches of at most n spans take the single-launch kernel (0: none); returns the previous value."""
+    return int(lib.crc32c_set_small_max(n))

@@ -1,31 +1,28 @@
 // crc32c_device.h -- CDNA4 (gfx950) device primitives for batched CRC-32C.
 //
-// Work model.  A group of LPI lanes (LPI = 64, 32 or 16; one wavefront holds
-// 64/LPI groups) owns one item span.  The span is cut into R rows of LPI * CH
-// bytes; lane i of the group owns bytes [i*CH, (i+1)*CH) of every row.  Each
-// lane runs R independent table-driven chains over its CH-byte chunks, folds
-// its R row partials with M_{LPI*CH}, and the LPI lane partials are merged by a
-// log2(LPI)-level reduction whose level k applies the fixed zeros operator
-// M_{CH*2^k}.  This is the algebra the reference uses to merge its three
-// crc32q streams (crc32c.c:184-220, zeros operators crc32c.c:85-137), widened
-// from 3 streams to LPI * R.
+// Work model.  A 32-lane group owns one item span (a wavefront holds two).
+// The span is cut into 4 KiB blocks of four 1 KiB rows; lane i of the group
+// owns bytes [32 i, 32 i + 32) of every row and runs one table-driven chain
+// per row.  The lane partials of a group are merged by a 5-level reduction
+// whose level k applies the fixed zeros operator M_{32 * 2^k}.  This is the
+// algebra the reference uses to merge its three crc32q streams
+// (crc32c.c:184-220, zeros operators crc32c.c:85-137), widened from 3 streams
+// to 128 per 4 KiB.
 //
-// Tables live in LDS, replicated once per bank of a 32-lane bank group so
-// every data lookup is conflict-free (lane l always reads bank l % 32):
-//
-//   SLICE == 1 (Sarwate, 64 KiB image, crc32c_gf2.h build_lds_image):
-//     row e (256 B): dwords [0,32) T0[e] x 32, dwords [32,64) aux slots.
-//   SLICE == 4 (slice-by-4, 156 KiB image, build_lds_image4):
-//     [0, 28 KiB)          aux tables, plain: table t entry e at t*1024 + e*4
-//     [28 KiB, +64 KiB)    row e: T3[e] x 32 | T2[e] x 32
-//     [92 KiB, +64 KiB)    row e: T1[e] x 32 | T0[e] x 32
-//   where Tk[b] = register after byte b then k zero bytes (crc32c.c:366-389).
+// Tables live in LDS.  The slice-by-4 tables are replicated once per bank of a
+// 32-lane bank group so every data lookup is conflict-free (lane l always
+// reads bank l % 32); the 160 KiB image (crc32c_gf2.h build_lds_image4/_k1):
+//   [0, 28 KiB)          aux tables, plain: table t entry e at t*1024 + e*4
+//   [28 KiB, +64 KiB)    row e: T3[e] x 32 | T2[e] x 32
+//   [92 KiB, +64 KiB)    row e: T1[e] x 32 | T0[e] x 32
+//   [156 KiB, 160 KiB)   K1: four more aux tables (row 0's shifted last step)
+// where Tk[b] = register after byte b then k zero bytes (crc32c.c:366-389).
 //
 // Aux tables hold the byte slices of zeros operators (crc32c.c:121-137 form);
 // operator o occupies aux tables 4o..4o+3:
-//   o = 0..5 : M_{CH * 2^o}  (lane-group reduction level o; for LPI = 32,
-//              o = 5 is M_{32*CH}, the row fold)
-//   o = 6    : M_{4 * 32 * CH} (4-row block fold of the span kernels)
+//   o = 0..4 : M_{32 * 2^o}  (lane-group reduction level o)
+//   o = 5, 6 : K1: the shifted last-step tables of rows 2 and 1
+//   span image: o = 4 is the 4 KiB block fold (level 4 = level 3 twice)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -34,18 +31,9 @@
 namespace mcrc_dev {
 
 constexpr uint32_t kAuxTree = 0;
-constexpr uint32_t kAuxOp5 = 20;  // M_{32*CH}
-constexpr uint32_t kAuxOp6 = 24;  // M_{128*CH}
-constexpr uint32_t kLdsImage1Bytes = 256 * 64 * 4;              // 64 KiB
-constexpr uint32_t kAux4Bytes = 28 * 1024;                        // 28 KiB
-constexpr uint32_t kLdsImage4Bytes = kAux4Bytes + 2 * 65536;     // 156 KiB
+constexpr uint32_t kAux4Bytes = 28 * 1024;  // 28 KiB of plain aux tables
 
 constexpr uint32_t kPoly = 0x82f63b78u;
-
-template <int SLICE>
-struct LdsImage {
-    static constexpr uint32_t bytes = SLICE == 1 ? kLdsImage1Bytes : kLdsImage4Bytes;
-};
 
 // The kernels declare no static LDS, so dynamic LDS starts at address 0 and a
 // byte offset is an LDS address (saves the base add hipcc emits for
@@ -65,35 +53,9 @@ struct LaneCtx {
 template <int SLICE>
 struct Step;
 
-// Sarwate: four dependent lookups per dword, 3 VALU + 1 LDS per byte.
-template <>
-struct Step<1> {
-    __device__ __forceinline__ static uint32_t byte1(uint32_t s, const LaneCtx &c) {
-        return lds_ld(__builtin_amdgcn_perm(s, c.lane4, 0x0c0c0400u)) ^ (s >> 8);
-    }
-    // x = register ^ little-endian data dword
-    __device__ __forceinline__ static uint32_t dword(uint32_t x, const LaneCtx &c) {
-        x = byte1(x, c);
-        x = byte1(x, c);
-        x = byte1(x, c);
-        return byte1(x, c);
-    }
-    __device__ __forceinline__ static uint32_t aux(uint32_t t, uint32_t e) {
-        // table t entry e: row 8t + (e >> 5), dword 32 + (e & 31)
-        return lds_ld((t << 11) | ((e & 0xe0u) << 3) | 128u | ((e & 31u) << 2));
-    }
-};
-
-// Slice-by-4: four independent lookups per dword, 2 VALU + 1 LDS per byte.
+// Slice-by-4 aux tables (plain, not replicated).
 template <>
 struct Step<4> {
-    __device__ __forceinline__ static uint32_t dword(uint32_t x, const LaneCtx &c) {
-        const uint32_t a3 = lds_ld(__builtin_amdgcn_perm(x, c.lane4, 0x0c0c0400u) + kAux4Bytes);
-        const uint32_t a2 = lds_ld(__builtin_amdgcn_perm(x, c.lane4, 0x0c0c0500u) + kAux4Bytes + 128u);
-        const uint32_t a1 = lds_ld(__builtin_amdgcn_perm(x, c.lane4hi, 0x0c020600u) + kAux4Bytes);
-        const uint32_t a0 = lds_ld(__builtin_amdgcn_perm(x, c.lane4hi, 0x0c020700u) + kAux4Bytes + 128u);
-        return (a3 ^ a2) ^ (a1 ^ a0);
-    }
     __device__ __forceinline__ static uint32_t aux(uint32_t t, uint32_t e) {
         return lds_ld((t << 10) | (e << 2));
     }
@@ -132,19 +94,6 @@ template <int SLICE>
 __device__ __forceinline__ uint32_t apply_op(uint32_t t0, uint32_t v) {
     return Step<SLICE>::aux(t0, v & 0xffu) ^ Step<SLICE>::aux(t0 + 1, (v >> 8) & 0xffu) ^
            Step<SLICE>::aux(t0 + 2, (v >> 16) & 0xffu) ^ Step<SLICE>::aux(t0 + 3, v >> 24);
-}
-
-// Merge the LPI lane partials of each lane group into the group's raw CRC,
-// which ends up in the group's first lane.  At level k only lanes with
-// i % 2^(k+1) == 0 look up their operator (fewer addresses compete for banks).
-template <int SLICE, int LPI>
-__device__ __forceinline__ uint32_t group_reduce(uint32_t v, uint32_t lane) {
-#pragma unroll
-    for (int k = 0; (1 << k) < LPI; ++k) {
-        const uint32_t x = __shfl_down(v, 1u << k, 64);
-        if ((lane & ((2u << k) - 1u)) == 0) v = apply_op<SLICE>(kAuxTree + 4 * k, v) ^ x;
-    }
-    return v;
 }
 
 // Value of lane (l + 2^k) for lanes whose partner stays inside a 32-lane
@@ -240,11 +189,6 @@ __device__ __forceinline__ uint32_t group_reduce32_span(uint32_t v, uint32_t lan
 __device__ __forceinline__ void load_tables(char *lds, const uint4 *__restrict__ img, uint32_t bytes) {
     uint4 *dst = reinterpret_cast<uint4 *>(lds);
     const uint32_t n = bytes / 16;
-#ifdef MCRC_TABLES_SERIAL  // (ablation: the one-load-per-iteration copy)
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = img[i];
-    __syncthreads();
-    return;
-#endif
     constexpr uint32_t U = 10;  // 160 KiB / (1024 threads x 16 B)
     for (uint32_t i0 = threadIdx.x; i0 < n; i0 += U * blockDim.x) {
         uint4 v[U];

@@ -142,7 +142,6 @@ inline uint32_t xpow8n_inv(uint64_t n) { return Gf2Op::zeros(n).inverse().apply(
 //   4o..4o+3: o <= 5 is M_{chunk * 2^o}, o = 6 is M_{128 * chunk}
 //   (the 4-row block fold of the span kernels).
 // ---------------------------------------------------------------------------
-constexpr int kImage1Dwords = 256 * 64;                    // SLICE 1: 64 KiB
 constexpr int kAux4Dwords = 28 * 256;                      // SLICE 4 aux: 28 KiB
 constexpr int kImage4Dwords = kAux4Dwords + 2 * 16384;     // SLICE 4: 156 KiB
 constexpr int kAuxTree = 0;
@@ -151,24 +150,6 @@ constexpr int kAuxFold = 24;
 inline void aux_ops(uint32_t chunk, Gf2Op ops[7]) {
     for (int k = 0; k < 6; ++k) ops[k] = Gf2Op::zeros((uint64_t)chunk << k);
     ops[6] = Gf2Op::zeros((uint64_t)chunk * 128);
-}
-
-inline void build_lds_image1(uint32_t *img, uint32_t chunk) {
-    memset(img, 0, sizeof(uint32_t) * kImage1Dwords);
-    uint32_t t0[256];
-    build_t0(t0);
-    for (int e = 0; e < 256; ++e)
-        for (int l = 0; l < 32; ++l) img[e * 64 + l] = t0[e];
-    Gf2Op ops[7];
-    aux_ops(chunk, ops);
-    for (int o = 0; o < 7; ++o) {
-        uint32_t tabs[4][256];
-        ops[o].byte_tables(tabs);
-        for (int k = 0; k < 4; ++k) {
-            const int t = 4 * o + k;
-            for (uint32_t e = 0; e < 256; ++e) img[(8 * t + (e >> 5)) * 64 + 32 + (e & 31)] = tabs[k][e];
-        }
-    }
 }
 
 inline void build_lds_image4(uint32_t *img, uint32_t chunk) {

@@ -1,27 +1,26 @@
 // crc32c_kernels.hip -- hand-written gfx950 kernels for batched CRC-32C.
 //
-// K1  k_fixed<SLICE, LPI, CH, R>: equal-length, 16-B aligned items at a fixed
-//     stride, len = R*LPI*CH (extstore spill batches of one slab class;
-//     BASELINE configs 2 and 4).  Replaces N calls of crc32c(0, item, len),
-//     crc32c_hw (crc32c.c:161-246) reached from storage.c:567.
+// K1  k_fixed<CRCIN>: equal 4 KiB, 16-B aligned items at a fixed stride
+//     (extstore spill batches of one slab class; BASELINE configs 2 and 4).
+//     Replaces N calls of crc32c(0, item, len), crc32c_hw (crc32c.c:161-246)
+//     reached from storage.c:567.
 // K2  k_spans<UNITS>: any offsets, lengths and alignment; one 32-lane group
 //     per work unit of <= 64 KiB (configs 3 and 5, storage.c:172 read-back
 //     spans), then k_final<MODE 0> per span.
-// K3  the same kernel over the spans of packed item images in extstore pages,
-//     [off+32, off+ITEM_ntotal) (k_count<MODE 1/2> parses the headers):
-//     k_final<MODE 1> checks the CRC stored in the item's exptime field
-//     (storage.c:160-178 over the page walk of storage.c:950-960);
+// K3  the same kernels over the spans of packed item images in extstore
+//     pages, [off+32, off+ITEM_ntotal) (k_count<MODE 1/2> parses the
+//     headers): k_final<MODE 1> checks the CRC stored in the item's exptime
+//     field (storage.c:160-178 over the page walk of storage.c:950-960);
 //     k_final<MODE 2> stamps it (the spill CRC of storage.c:567, batched per
-//     wbuf).
+//     wbuf).  k_walk walks the pages on the device.
+// K4  k_blocks: spans whose unit is one 4 KiB block (K1's loop, gathered).
+//     k_small: batches of up to 8192 spans in one launch (IO batches, wbufs,
+//     the coalescing queue).
 //
 // See crc32c_device.h for the lane-group work model and LDS table layouts.
 #include "crc32c_device.h"
 
 namespace mcrc_dev {
-
-#ifdef MCRC_UBENCH_CLOCK  // dev tool (tools/ubench.hip): per-block core clock vs wall clock
-__device__ uint64_t *g_clock_stamps;
-#endif
 
 // ===========================================================================
 // K1: fixed-length aligned items
@@ -40,7 +39,7 @@ template <int LPI, int CH, int R>
 struct ItemRegs {
     static constexpr int Q = CH / 16;
     uint4 d[R][Q];
-    uint32_t cin;  // MODE 11: the item's initial CRC
+    uint32_t cin;  // the item's initial CRC
 
     __device__ __forceinline__ void load(const uint8_t *__restrict__ p, uint32_t li) {
 #pragma unroll
@@ -56,69 +55,12 @@ struct ItemRegs {
 #pragma unroll
             for (int q = 0; q < Q; ++q) d[r][q] = ld16(wb + loff + (r * LPI * CH + 16 * q));
     }
-    __device__ __forceinline__ uint32_t checksum() const {
-        uint32_t a = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int q = 0; q < Q; ++q) a ^= d[r][q].x ^ d[r][q].y ^ d[r][q].z ^ d[r][q].w;
-        return a;
-    }
 };
 
-// Lane partial: R independent chains (interleaved dword by dword for ILP),
-// folded with M_{LPI*CH} into the raw CRC of the lane's R chunks as placed in
-// the item.  FOLD=false is a profiling ablation.
-template <int SLICE, int LPI, int CH, int R, bool FOLD = true>
-__device__ __forceinline__ uint32_t lane_partial(const ItemRegs<LPI, CH, R> &it, const LaneCtx &c) {
-    constexpr int Q = CH / 16;
-    constexpr uint32_t kFold = 4 * (LPI == 64 ? 6 : LPI == 32 ? 5 : 4);  // M_{LPI*CH}
-    uint32_t s[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) s[r] = 0;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const uint4 &v = it.d[r][q];
-                const uint32_t w = k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
-                s[r] = Step<SLICE>::dword(s[r] ^ w, c);
-            }
-        }
-    }
-    uint32_t a = s[0];
-#pragma unroll
-    for (int r = 1; r < R; ++r) a = (FOLD ? apply_op<SLICE>(kFold, a) : a) ^ s[r];
-    return a;
-}
-
-// Lane partial for SLICE 4, LPI 32: chains fused with bitop3 XORs.
-template <int CH, int R, bool FOLD = true>
-__device__ __forceinline__ uint32_t lane_partial_x3(const ItemRegs<32, CH, R> &it, const LaneCtx &c) {
-    constexpr int Q = CH / 16;
-    constexpr int N = 4 * Q;  // dwords per chain
-    uint32_t x[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = it.d[r][0].x;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t wn = i + 1 < N ? dw4(it.d[r][(i + 1) >> 2], (i + 1) & 3) : 0u;
-            x[r] = step4_next(x[r], wn, c);
-        }
-    }
-    uint32_t a = x[0];
-#pragma unroll
-    for (int r = 1; r < R; ++r) a = (FOLD ? apply_op<4>(kAuxOp5, a) : a) ^ x[r];
-    return a;
-}
-
-// lane_partial_x3 for R = 4 on the K1 image: the last step of row chains 0..2
-// reads the shifted tables (row fold included), so the lane partial is the
-// XOR of the four chains -- no fold operators.
+// Lane partial of a 32-lane group on the K1 image: four row chains (slice-by-4,
+// interleaved dword by dword for ILP, two v_bitop3 per step); the last step of
+// row chains 0..2 reads the shifted tables (the row fold M_{(3-r)*1024}
+// included), so the lane partial is the XOR of the four chains.
 template <int CH>
 __device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &it, const LaneCtx &c) {
     constexpr int Q = CH / 16;
@@ -141,78 +83,32 @@ __device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &
     return xor3(x[0], x[1], x[2]) ^ x[3];
 }
 
-// Same as lane_partial_x3, but the loads of the NEXT step (into `nxt`) are
-// issued one at a time between dword steps of this chain, so the vector
-// memory queue is fed steadily instead of in one burst per step.
-template <int CH, int R>
-__device__ __forceinline__ uint32_t lane_partial_x3_feed(const ItemRegs<32, CH, R> &it, const LaneCtx &c,
-                                                         ItemRegs<32, CH, R> &nxt, const uint8_t *np,
-                                                         uint32_t li) {
-    constexpr int Q = CH / 16;
-    constexpr int N = 4 * Q;       // dwords per chain
-    constexpr int NL = R * Q;      // loads per step
-    constexpr int EVERY = N / NL > 0 ? N / NL : 1;
-    uint32_t x[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) x[r] = it.d[r][0].x;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        if (i % EVERY == 0 && i / EVERY < NL) {
-            constexpr int dummy = 0;
-            (void)dummy;
-            const int l = i / EVERY, r = l / Q, q = l % Q;
-            nxt.d[r][q] = ld16(np + (size_t)r * 32 * CH + li * CH + 16 * q);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t wn = i + 1 < N ? dw4(it.d[r][(i + 1) >> 2], (i + 1) & 3) : 0u;
-            x[r] = step4_next(x[r], wn, c);
-        }
-    }
-#pragma unroll
-    for (int l = (N + EVERY - 1) / EVERY; l < NL; ++l) {
-        const int r = l / Q, q = l % Q;
-        nxt.d[r][q] = ld16(np + (size_t)r * 32 * CH + li * CH + 16 * q);
-    }
-    uint32_t a = x[0];
-#pragma unroll
-    for (int r = 1; r < R; ++r) a = apply_op<4>(kAuxOp5, a) ^ x[r];
-    return a;
-}
+// K1 geometry: a 32-lane group owns one 4096-B item (4 rows of 1 KiB, lane i
+// owns bytes [32 i, 32 i + 32) of each row), a wave two items per step.
+constexpr uint32_t kK1Rows = 4, kK1CH = 32, kK1Bytes = kK1Rows * 32 * kK1CH;
 
-// Persistent grid-stride loop; each wave handles 64/LPI items per step and
-// loads the next step's items before reducing the current ones (register
-// ping-pong, no copies).
-//   out[i] = crc32c(crc_in ? crc_in[i] : 0, base + i*stride, len),  len = R*LPI*CH
-//   kfinal = ~M_len(0xffffffff), kspan = x^(8*len) mod P.
-// MODE 0: full CRC.  Ablations for profiling (wrong results by design):
-// MODE 1: loads only; MODE 2: no lane-group reduction; MODE 3: data chains only.
-// MODE 4/5: full CRC, optimised variants (SLICE 4, LPI 32 only).
-// MODE 6: MODE 5 with the next step's loads spread over the chains.
-// MODE 7: MODE 5 chains without row folds or lane reduction (ablation).
-// MODE 9/10: MODE 1 plus s_sleep 20/40 per step (ablation: compute-like gaps).
-// MODE 11: MODE 5 with ~crc_in injected into the first data dword (CRCIN:
-//          crc_in[] is loaded with the item; otherwise crc_in = 0).
-// PRIO > 0: the wave raises its issue priority while it issues loads.
-template <int SLICE, int LPI, int CH, int R, int MODE, int DEPTH = 2, int STAGGER = 0, int PRIO = 0,
-          bool SCHED_FENCE = false, bool CRCIN = false>
+// Persistent grid-stride loop over equal 4 KiB items at a fixed stride:
+//   out[i] = crc32c(crc_in ? crc_in[i] : 0, base + i * stride, 4096).
+// Per item: ~crc_in is XORed into the item's first data dword (a register
+// seeded with ~crc_in adds exactly M_len(~crc_in), crc32c.c:166, so
+// crc32c(crc_in, D) = ~raw(D ^ (~crc_in || 0...)) -- no multiply), the lane
+// partials are the four row chains' XOR, and four consecutive steps of the
+// wave are reduced by one lane tree (group_pair_level1 + group_reduce32_quad).
+// Loads run one step ahead in two register sets (no copies).
+template <bool CRCIN>
 __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base, uint64_t stride,
                                                 uint64_t nitems, const uint4 *__restrict__ img,
-                                                uint32_t kfinal, uint32_t kspan,
                                                 const uint32_t *__restrict__ crc_in,
                                                 uint32_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    load_tables(smem, img, MODE >= 13 ? kLdsImageK1Bytes : LdsImage<SLICE>::bytes);
-#ifdef MCRC_UBENCH_CLOCK
-    const uint64_t clk0 = clock64(), wall0 = wall_clock64();
-#endif
-    constexpr uint32_t IPW = 64 / LPI;
+    load_tables(smem, img, kLdsImageK1Bytes);
+    using Regs = ItemRegs<32, kK1CH, kK1Rows>;
+    constexpr uint32_t IPW = 2;  // items per wave and step
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t li = lane % LPI;
-    const uint32_t g = lane / LPI;
+    const uint32_t li = lane & 31u;
+    const uint32_t g = lane >> 5;
     LaneCtx c;
-    c.lane4 = (lane & 31u) << 2;
+    c.lane4 = li << 2;
     c.lane4hi = c.lane4 | 0x10000u;
     const uint64_t waves = blockDim.x >> 6;
     const uint64_t gstep = gridDim.x * waves;
@@ -223,211 +119,70 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // which drained the prefetched step).
     uint64_t grp = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
     if (grp >= ngroups) return;
-    if constexpr (STAGGER > 0) {
-        // desynchronise the workgroup's waves: odd waves start STAGGER x 8K cycles late
-        if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 1u)
-            for (int i = 0; i < STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-
     auto item_of = [&](uint64_t gi) { return gi * IPW + g; };
-    auto clamp = [&](uint64_t it) { return it < nitems ? it : nitems - 1; };
-    auto finish = [&](const ItemRegs<LPI, CH, R> &regs, uint64_t gi) {
-        const uint64_t item = item_of(gi);
-        if (MODE == 1 || MODE == 9 || MODE == 10) {
-            const uint32_t a = regs.checksum();
-            if (MODE == 9) __builtin_amdgcn_s_sleep(20);
-            if (MODE == 10) __builtin_amdgcn_s_sleep(40);
-            if (a == 0x9e3779b9u && item < nitems) out[item] = a;
-            return;
-        }
-        uint32_t raw;
-        if (MODE == 11) {
-            // ~crc_in injected into the item's first dword: a register seeded
-            // with ~crc_in adds exactly M_len(~crc_in) (crc32c.c:166), so
-            // crc32c(crc_in, D) = ~raw(D ^ (~crc_in || 0...)) -- no multiply.
-            ItemRegs<LPI, CH, R> &m = const_cast<ItemRegs<LPI, CH, R> &>(regs);
-            if (li == 0) m.d[0][0].x ^= ~m.cin;
-            raw = group_reduce32_dpp(lane_partial_x3<CH, R>(m, c), lane);
-            if (li == 0 && item < nitems) out[item] = ~raw;
-            return;
-        }
-        if (MODE == 5)  // optimised: bitop3 chains + DPP reduction (SLICE 4, LPI 32)
-            raw = group_reduce32_dpp(lane_partial_x3<CH, R>(regs, c), lane);
-        else if (MODE == 7)
-            raw = lane_partial_x3<CH, R, false>(regs, c);
-        else if (MODE == 4)  // bitop3 chains, LDS-shuffle reduction
-            raw = group_reduce<SLICE, LPI>(lane_partial_x3<CH, R>(regs, c), lane);
-        else if (MODE == 3)
-            raw = lane_partial<SLICE, LPI, CH, R, false>(regs, c);
-        else if (MODE == 2)
-            raw = lane_partial<SLICE, LPI, CH, R>(regs, c);
-        else
-            raw = group_reduce<SLICE, LPI>(lane_partial<SLICE, LPI, CH, R>(regs, c), lane);
-        if (li == 0 && item < nitems) {
-            out[item] = crc_in ? ~(mulmodp_dev(~crc_in[item], kspan) ^ raw) : raw ^ kfinal;
-        }
-    };
 
-    auto addr = [&](uint64_t gi) { return base + clamp(item_of(gi < ngroups ? gi : ngroups - 1)) * stride; };
-    ItemRegs<LPI, CH, R> ra, rb;
-    // The sched_barrier keeps the next step's loads at the top of the step:
-    // left alone, the scheduler sinks them into the chains (to shorten their
-    // live ranges), so the following step waits on loads issued moments before.
-    auto ld = [&](ItemRegs<LPI, CH, R> &r, uint64_t gi) {
-        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
-        if constexpr (MODE >= 11) {
-            // uniform step base + per-lane offset: no 64-bit VGPR address math
-            // (and no fresh temporaries) at the top of a step
-            // A wave's last prefetch runs one step past its last group; it
-            // re-reads that group (just loaded, cache-hot) -- clamping every
-            // wave to the batch's last group made 4096 waves read the same
-            // 8 KiB at the end of the launch.
-#ifdef MCRC_K1_CLAMP_LAST  // (ablation: the old clamp)
-            const uint64_t gu = gi < ngroups ? gi : ngroups - 1;
-#else
-            const uint64_t gu = gi < ngroups ? gi : gi - gstep < ngroups ? gi - gstep : ngroups - 1;
-#endif
-            const uint64_t first = gu * IPW;
-            const uint8_t *wb = base + first * stride;
-            const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
-            // crc_in first: it is consumed before the first chain step, and
-            // vmcnt counts in issue order (issued last, it made the step wait
-            // for all of its loads before any chain could start)
-            if constexpr (CRCIN) r.cin = crc_in[first + gl];
-            else r.cin = 0u;
-            r.load_at(wb, gl * (uint32_t)stride + li * CH);
-        } else {
-            r.load(addr(gi), li);
-        }
-        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
-        if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
+    Regs ra, rb;
+    // Uniform step base + per-lane offset: no 64-bit VGPR address math at the
+    // top of a step.  A wave's last prefetch runs one step past its last
+    // group; it re-reads that group (just loaded, cache-hot) -- clamping every
+    // wave to the batch's last group made 4096 waves read the same 8 KiB at
+    // the end of the launch.  The sched_barrier keeps the loads at the top of
+    // the step: left alone, the scheduler sinks them into the chains and the
+    // next step waits on loads issued moments before.
+    auto ld = [&](Regs &r, uint64_t gi) {
+        const uint64_t gu = gi < ngroups ? gi : gi - gstep < ngroups ? gi - gstep : ngroups - 1;
+        const uint64_t first = gu * IPW;
+        const uint8_t *wb = base + first * stride;
+        const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
+        // crc_in first: it is consumed before the first chain step, and
+        // vmcnt counts in issue order (issued last, it made the step wait for
+        // all of its loads before any chain could start)
+        if constexpr (CRCIN) r.cin = crc_in[first + gl];
+        else r.cin = 0u;
+        r.load_at(wb, gl * (uint32_t)stride + li * kK1CH);
+        __builtin_amdgcn_sched_barrier(0);
     };
-    if constexpr (MODE == 6) {
-        // loads of the next step interleaved with this step's chains
-        auto fin6 = [&](const ItemRegs<LPI, CH, R> &cur, ItemRegs<LPI, CH, R> &nxt, uint64_t gi) {
-            const uint64_t item = item_of(gi);
-            const uint32_t raw =
-                group_reduce32_dpp(lane_partial_x3_feed<CH, R>(cur, c, nxt, addr(gi + gstep), li), lane);
-            if (li == 0 && item < nitems)
-                out[item] = crc_in ? ~(mulmodp_dev(~crc_in[item], kspan) ^ raw) : raw ^ kfinal;
-        };
-        ra.load(addr(grp), li);
-        for (;;) {
-            fin6(ra, rb, grp);
-            grp += gstep;
-            if (grp >= ngroups) break;
-            fin6(rb, ra, grp);
-            grp += gstep;
-            if (grp >= ngroups) break;
-        }
-    } else if (DEPTH == 2 && (MODE == 12 || MODE == 13 || MODE == 14)) {
-        // MODE 11 with the two steps of an iteration reduced together
-        // (group_reduce32_pair): per item pair, 1 + 1 + 4 reduction levels
-        // instead of 2 x 5.  MODE 13: row folds inside the chains' last step
-        // (lane_partial_x3s, K1 image).  MODE 14: MODE 13 with four steps per
-        // iteration reduced together (group_reduce32_quad).
-        auto lp = [&](const ItemRegs<LPI, CH, R> &m) {
-            if constexpr (MODE >= 13) return lane_partial_x3s<CH>(m, c);
-            else return lane_partial_x3<CH, R>(m, c);
-        };
-        auto part0 = [&](ItemRegs<LPI, CH, R> &m) {
-            if (li == 0) m.d[0][0].x ^= ~m.cin;
-            const uint32_t p = lp(m);
-            return reduce_level<0>(p, (lane & 1u) == 0u);
-        };
-        auto fin11 = [&](ItemRegs<LPI, CH, R> &m, uint64_t gi) {
-            if (li == 0) m.d[0][0].x ^= ~m.cin;
-            const uint32_t raw = group_reduce32_dpp(lp(m), lane);
-            const uint64_t item = item_of(gi);
-            if (li == 0 && item < nitems) out[item] = ~raw;
-        };
-        const uint64_t nsteps = (ngroups - grp + gstep - 1) / gstep;
-        ld(ra, grp);
-        uint64_t k = 0;
-        if constexpr (MODE == 14) {
-            for (; k + 4 <= nsteps; k += 4) {
-                ld(rb, grp + gstep);
-                const uint32_t va = part0(ra);
-                ld(ra, grp + 2 * gstep);
-                const uint32_t vb = part0(rb);
-                const uint32_t vab = group_pair_level1(va, vb, lane);
-                ld(rb, grp + 3 * gstep);
-                const uint32_t vc = part0(ra);
-                ld(ra, grp + 4 * gstep);
-                const uint32_t vd = part0(rb);
-                const uint32_t raw = group_reduce32_quad(vab, group_pair_level1(vc, vd, lane), lane);
-                const uint64_t item = item_of(grp + (li & 3u) * gstep);
-                if (li < 4 && item < nitems) out[item] = ~raw;
-                grp += 4 * gstep;
-            }
-        }
-        for (; k + 2 <= nsteps; k += 2) {
-            ld(rb, grp + gstep);
-            const uint32_t va = part0(ra);
-            ld(ra, grp + 2 * gstep);
-            const uint32_t vb = part0(rb);
-            const uint32_t raw = group_reduce32_pair(va, vb, lane);
-            const uint64_t item = item_of(li == 0 ? grp : grp + gstep);
-            if (li < 2 && item < nitems) out[item] = ~raw;
-            grp += 2 * gstep;
-        }
-        if (nsteps & 1) fin11(ra, grp);
-    } else if (DEPTH == 2 && MODE == 11) {
-        // One exit, at the bottom: a break between the two halves would give
-        // the loop header a second (un-waited) predecessor, and the waitcnt
-        // pass would then drain every prefetched load there.
-        const uint64_t nsteps = (ngroups - grp + gstep - 1) / gstep;
-        ld(ra, grp);
-        for (uint64_t k = 0; k + 2 <= nsteps; k += 2) {
-            ld(rb, grp + gstep);
-            finish(ra, grp);
-            grp += gstep;
-            ld(ra, grp + gstep);
-            finish(rb, grp);
-            grp += gstep;
-        }
-        if (nsteps & 1) finish(ra, grp);
-    } else if (DEPTH == 2) {
-        ld(ra, grp);
-        for (;;) {
-            ld(rb, grp + gstep);
-            finish(ra, grp);
-            grp += gstep;
-            if (grp >= ngroups) break;
-            ld(ra, grp + gstep);
-            finish(rb, grp);
-            grp += gstep;
-            if (grp >= ngroups) break;
-        }
-    } else {
-        // three register buffers: two steps in flight while one is reduced
-        ItemRegs<LPI, CH, R> rc;
-        ld(ra, grp);
+    auto part0 = [&](Regs &m) {
+        if (li == 0) m.d[0][0].x ^= ~m.cin;
+        return reduce_level<0>(lane_partial_x3s<kK1CH>(m, c), (lane & 1u) == 0u);
+    };
+    // One exit, at the bottom of each loop: a break between the halves would
+    // give the loop header a second (un-waited) predecessor, and the waitcnt
+    // pass would then drain every prefetched load there.
+    const uint64_t nsteps = (ngroups - grp + gstep - 1) / gstep;
+    ld(ra, grp);
+    uint64_t k = 0;
+    for (; k + 4 <= nsteps; k += 4) {
         ld(rb, grp + gstep);
-        for (;;) {
-            ld(rc, grp + 2 * gstep);
-            finish(ra, grp);
-            grp += gstep;
-            if (grp >= ngroups) break;
-            ld(ra, grp + 2 * gstep);
-            finish(rb, grp);
-            grp += gstep;
-            if (grp >= ngroups) break;
-            ld(rb, grp + 2 * gstep);
-            finish(rc, grp);
-            grp += gstep;
-            if (grp >= ngroups) break;
-        }
+        const uint32_t va = part0(ra);
+        ld(ra, grp + 2 * gstep);
+        const uint32_t vb = part0(rb);
+        const uint32_t vab = group_pair_level1(va, vb, lane);
+        ld(rb, grp + 3 * gstep);
+        const uint32_t vc = part0(ra);
+        ld(ra, grp + 4 * gstep);
+        const uint32_t vd = part0(rb);
+        const uint32_t raw = group_reduce32_quad(vab, group_pair_level1(vc, vd, lane), lane);
+        const uint64_t item = item_of(grp + (li & 3u) * gstep);
+        if (li < 4 && item < nitems) out[item] = ~raw;
+        grp += 4 * gstep;
     }
-#ifdef MCRC_UBENCH_CLOCK
-    if (threadIdx.x == 0) {
-        const uint64_t clk1 = clock64(), wall1 = wall_clock64();
-        g_clock_stamps[4 * blockIdx.x + 0] = clk0;
-        g_clock_stamps[4 * blockIdx.x + 1] = clk1;
-        g_clock_stamps[4 * blockIdx.x + 2] = wall0;
-        g_clock_stamps[4 * blockIdx.x + 3] = wall1;
+    for (; k + 2 <= nsteps; k += 2) {
+        ld(rb, grp + gstep);
+        const uint32_t va = part0(ra);
+        ld(ra, grp + 2 * gstep);
+        const uint32_t vb = part0(rb);
+        const uint32_t raw = group_reduce32_pair(va, vb, lane);
+        const uint64_t item = item_of(li == 0 ? grp : grp + gstep);
+        if (li < 2 && item < nitems) out[item] = ~raw;
+        grp += 2 * gstep;
     }
-#endif
+    if (nsteps & 1) {
+        if (li == 0) ra.d[0][0].x ^= ~ra.cin;
+        const uint32_t raw = group_reduce32_dpp(lane_partial_x3s<kK1CH>(ra, c), lane);
+        const uint64_t item = item_of(grp);
+        if (li == 0 && item < nitems) out[item] = ~raw;
+    }
 }
 
 // ===========================================================================
@@ -473,10 +228,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 constexpr uint32_t kSpanCH = 32;
 constexpr uint32_t kRowBytes = 32 * kSpanCH;  // 1024
 constexpr uint32_t kBlockBytes = 4 * kRowBytes;  // 4096
-#ifndef MCRC_SEG_KIB
-#define MCRC_SEG_KIB 64
-#endif
-constexpr uint32_t kSegBytes = MCRC_SEG_KIB * 1024;
+constexpr uint32_t kSegBytes = 64 * 1024;  // (16-256 KiB measured; 24-64 KiB alike)
 constexpr uint32_t kWhole = 0xffffffffu;      // unit segment index: the whole span
 // Pieces outside a span are read from a zeroed buffer; workgroup b reads the
 // 16 B at zero + 4 KiB * (b % 256), so the workgroups' zero reads spread over
@@ -508,6 +260,8 @@ struct SpanArgs {
     uint32_t *span_acc;        // planned batches: R per span (segment units XOR their shifted values in)
     const uint32_t *segpow;    // rows k (x^i * x^(8 * 64Ki * k), i < 32) for k < 256, then k = 256 j
     uint64_t region;           // MODE 1: items never cross a multiple of `region` (0: no bound)
+    uint32_t cfl;              // MODE 1/2: bytes of the ITEM_CFLAGS suffix, sizeof(client_flags_t):
+                               // 4, or 8 in a LARGE_CLIENT_FLAGS build (memcached.h:96-100)
     // k_small only (nullptr: nbad is the caller's to zero and read): the last
     // workgroup moves *nbad to this pinned host word and zeroes *nbad and *done
     unsigned long long *host_nbad;
@@ -638,10 +392,7 @@ __device__ __forceinline__ Piece clear_below(Piece v, uint32_t k) {
 // (leading zeros leave a zero register unchanged), so
 //   r' = M_m(r) ^ raw16(the m bytes at the top).
 // Every load is an aligned piece holding a byte of [p, p + n).
-#ifndef MCRC_ADV_UNROLL
-#define MCRC_ADV_UNROLL 4
-#endif
-constexpr int kAdvUnroll = MCRC_ADV_UNROLL;
+constexpr int kAdvUnroll = 4;
 __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, uint32_t n, const Tab8 &t) {
     if (n == 0) return r;
     const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
@@ -671,14 +422,8 @@ __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, ui
 // (The limits are measured: a thread's chain is serial, one LDS round trip
 // per 16 B, so long fragments cost more than the block step they save --
 // DESIGN.md section 3.)
-#ifndef MCRC_FRAG_MAX
-#define MCRC_FRAG_MAX 128
-#endif
-#ifndef MCRC_WHOLE_MAX
-#define MCRC_WHOLE_MAX 1024
-#endif
-constexpr uint32_t kFragMax = MCRC_FRAG_MAX;    // a head fragment [p, G1) of at most this
-constexpr uint32_t kWholeMax = MCRC_WHOLE_MAX;  // a whole span of vlen at most this
+constexpr uint32_t kFragMax = 128;    // a head fragment [p, G1) of at most this
+constexpr uint32_t kWholeMax = 1024;  // a whole span of vlen at most this
 static_assert(kWholeMax + 16 <= kBlockBytes, "a whole span held by its thread is its own fragment (G1 = Ea)");
 // Is the head fragment (G1 - p = g1o) the span thread's?  For vlen <= kWholeMax
 // the fragment is the whole span (G1 = Ea).
@@ -757,8 +502,9 @@ struct ItemHdr {
     uint32_t nbytes;   // 32..35
     uint32_t flags;    // it_flags, 38..39
     uint32_t nkey;     // 41
-    __device__ __forceinline__ uint64_t ntotal() const {
-        return 48ull + nkey + 1 + nbytes + ((flags & 256u) ? 4 : 0) + ((flags & 2u) ? 8 : 0);
+    // cfl = sizeof(client_flags_t) (SpanArgs::cfl)
+    __device__ __forceinline__ uint64_t ntotal(uint32_t cfl) const {
+        return 48ull + nkey + 1 + nbytes + ((flags & 256u) ? cfl : 0) + ((flags & 2u) ? 8 : 0);
     }
 };
 __device__ __forceinline__ ItemHdr parse_hdr(const uint8_t *it) {
@@ -781,7 +527,7 @@ __device__ __forceinline__ ItemHdr parse_hdr(const uint8_t *it) {
 // stored CRC in aux.
 __device__ __forceinline__ ItemDesc item_desc(const SpanArgs &a, uint64_t off, const ItemHdr &h, bool hdr_ok) {
     ItemDesc d;
-    const uint64_t ntotal = h.ntotal();
+    const uint64_t ntotal = h.ntotal(a.cfl);
     d.aux = h.exptime;
     // an item never crosses its write buffer (extstore.c:627-636), so a
     // header claiming otherwise is corrupt
@@ -1005,13 +751,10 @@ __device__ __forceinline__ uint32_t mul_row_group(uint32_t v0, uint32_t xi, uint
     return term;
 }
 
-#ifndef MCRC_SPAN_BLOCK
-#define MCRC_SPAN_BLOCK 1024
-#endif
 // 16 waves per CU (128 VGPRs).  768 threads (168 VGPRs) measured slower
 // (config 3: 5.99 vs 5.90 ms; config 5: 6.90 vs 5.93 ms per 300 pages):
 // latency hiding of the dependent lookup chains needs the waves.
-constexpr uint32_t kSpanBlock = MCRC_SPAN_BLOCK;
+constexpr uint32_t kSpanBlock = 1024;
 
 // The span kernel: R = raw([ph, e)) of every work unit, pieces as they lie.
 // A unit that is a whole span stores R (span_acc[span], or out[span] without
@@ -1046,11 +789,7 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
     uint32_t k = 0;    // block index inside cur
     uint32_t acc = 0;  // lane accumulator over the blocks of cur
     BlockWin w0, w1;
-#ifdef MCRC_ZERO_SINGLE  // (ablation: one zero line for every workgroup)
-    const uint4 *zero = a.zero;
-#else
     const uint4 *zero = a.zero + (blockIdx.x % kZeroSlots) * (4096 / 16);
-#endif
     load_block(w0, cur, 0, li, zero);
 
     // Process the block held in `w` (block k of cur) after issuing the loads of
@@ -1101,20 +840,12 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
                                    : __all(grel + (int32_t)kRowBytes <= 0)     ? 1u
                                                                                : 0u;
             uint32_t v;
-#ifdef MCRC_ABL_LOADS_ONLY  // ablation: no chains (wrong CRCs): the loads and the per-unit work only
-            v = 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v ^= w.v[r][0].x ^ w.v[r][0].y ^ w.v[r][0].z ^ w.v[r][0].w ^ w.v[r][1].x ^
-                                           w.v[r][1].y ^ w.v[r][1].z ^ w.v[r][1].w;
-            if (nskip == 7) v = 1;
-#else
             switch (nskip) {
                 case 0: v = block_value<0>(w, c); break;
                 case 1: v = block_value<1>(w, c); break;
                 case 2: v = block_value<2>(w, c); break;
                 default: v = block_value<3>(w, c); break;
             }
-#endif
             // (the fold of a unit's first block is of acc = 0: skipped when no
             // group of the wave is past its first block, e.g. one-block units)
             if (__builtin_amdgcn_readfirstlane(__any(k != 0))) acc = apply_op<4>(kAuxSpanFold, acc);
@@ -1122,11 +853,7 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         }
         if (last) {
             if (cur.valid()) {
-#ifdef MCRC_ABL_NOTREE  // ablation: no lane-group tree (wrong CRCs)
-                const uint32_t raw = acc;
-#else
                 const uint32_t raw = group_reduce32_span(acc, lane);
-#endif
                 if (!UNITS) {
                     if (li == 0) a.out[u] = raw;
                 } else {
@@ -1414,7 +1141,15 @@ __global__ __launch_bounds__(1024) void k_small(SpanArgs a, const uint4 *__restr
     // one atomic per wave with a bad span (all 160 KiB of LDS hold the tables,
     // so no workgroup-level sum as in count_bad)
     const uint64_t m = __ballot(nb != 0);
-    if (m && lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) atomicAdd(a.nbad, (unsigned long long)__popcll(m));
+    if (m && lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) {
+        atomicAdd(a.nbad, (unsigned long long)__popcll(m));
+        // the add must be performed before this workgroup is counted done:
+        // __syncthreads is a workgroup-scope release and does not wait for
+        // another wave's outstanding global atomics, so without this fence
+        // the last workgroup could read nbad before the add lands (a lost
+        // count this call, a phantom one the next)
+        __threadfence();
+    }
     if (a.host_nbad) {
         // the last workgroup to finish hands the count to the host and leaves
         // the counters at zero for the next call: no memset before the launch
@@ -1608,10 +1343,7 @@ __global__ void k_chain(const uint32_t *iov_crc, const uint32_t *lens, uint32_t 
 // on from lane m's item end with s = its ntotal.  Whatever the data, the
 // result is the sequential walk's (tests/test_walk_model.py restates it);
 // equal-sized items cost one round trip per 64 of them.
-#ifndef MCRC_WALK_WAVES
-#define MCRC_WALK_WAVES 4
-#endif
-constexpr uint32_t kWalkWaves = MCRC_WALK_WAVES;  // waves (wbufs) per workgroup
+constexpr uint32_t kWalkWaves = 4;  // waves (wbufs) per workgroup
 
 struct WalkOut {
     uint32_t *cnt;           // count pass: items per wbuf
@@ -1647,7 +1379,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
             const bool in = (j == 0 || s != 0) && o + 48 <= size;  // (s < 2^33: no overflow)
             ItemHdr h{0u, 0u, 0u, 0u};
             if (in) h = parse_hdr(wb + o);
-            const uint64_t nt = h.ntotal();
+            const uint64_t nt = h.ntotal(a.cfl);
             const bool item = in && h.nkey != 0;
             // m = the first lane whose successor's guess is wrong (64: none)
             const uint64_t brk = __ballot(!(item && nt == s));

@@ -14,6 +14,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -52,15 +54,12 @@ namespace {
 
 constexpr int kBlock = 1024;                    // 16 waves, 32 lane groups
 constexpr uint32_t kItemsPerBlockStep = 32;     // one span per 32-lane group
-constexpr uint32_t kFixedLen = 4096;            // K1 instance: 4 rows x 32 lanes x 32 B
-constexpr uint32_t kFixedCH = 32;
-static_assert(kFixedCH == mcrc_dev::kSpanCH, "K1 and the span kernels share one table image");
-// K1: MODE 14 (crc_in injected into the first data dword, row folds inside the
-// chains' last step via the K1 image, four steps reduced together), loads
-// fenced at the top of each step; CRCIN selects the instance that reads crc_in[].
-#define K1_KERNEL(CRCIN) mcrc_dev::k_fixed<4, 32, kFixedCH, 4, 14, 2, 0, 0, true, CRCIN>
+constexpr uint32_t kFixedLen = mcrc_dev::kK1Bytes;  // K1: 4 rows x 32 lanes x 32 B
+static_assert(mcrc_dev::kK1CH == mcrc_dev::kSpanCH, "K1 and the span kernels share one table image");
 
 thread_local float g_last_kernel_ms = -1.0f;
+
+struct Queue;
 
 struct Device {
     int id = -1;
@@ -80,7 +79,8 @@ struct Device {
     hipStream_t stream = nullptr, copy = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};  // host-batch pipeline slots
-    std::mutex mu;              // serialises every entry point on this device
+    std::mutex mu;              // serialises the entry points that use the scratch below
+    Queue *queue = nullptr;     // coalescing queue (crc32c_batch_submit), created on first use
     // Shared device scratch (plan buffers, nbad, walk buffers) is owned in
     // stream order: a launch on stream B waits for the last use on stream A.
     hipEvent_t busy = nullptr;
@@ -131,8 +131,32 @@ struct Device {
         }
         return s.p;
     }
+    // grow-only pinned, device-mapped scratch of the host item-image calls:
+    // host address in *h, the address kernels use in *dv
+    struct Pinned {
+        void *h = nullptr, *d = nullptr;
+        size_t bytes = 0;
+    } pinned[4];
+    bool grow_pinned(int slot, size_t bytes, void **h, void **dv) {
+        Pinned &s = pinned[slot];
+        if (s.bytes < bytes) {
+            if (s.h) (void)hipHostFree(s.h);
+            s = Pinned{};
+            if (hipHostMalloc(&s.h, bytes, hipHostMallocDefault) != hipSuccess) return false;
+            if (hipHostGetDevicePointer(&s.d, s.h, 0) != hipSuccess) {
+                (void)hipHostFree(s.h);
+                s = Pinned{};
+                return false;
+            }
+            s.bytes = bytes;
+        }
+        *h = s.h;
+        *dv = s.d;
+        return true;
+    }
 };
-enum { kScrWalkCnt, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage };
+enum { kScrWalkCnt, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage, kScrItemOffs, kScrItemOut };
+enum { kPinStage, kPinOffs, kPinOk, kPinCrc };
 
 std::mutex g_dev_mu;
 std::vector<std::unique_ptr<Device>> g_devs;
@@ -194,7 +218,7 @@ int init_device(Device &d, int id) {
     HIP_OK(hipMalloc(&d.tab8, tab8.size() * 4));
     HIP_OK(hipMemcpy(d.tab8, tab8.data(), tab8.size() * 4, hipMemcpyHostToDevice));
     std::vector<uint32_t> img_k1(mcrc::kImageK1Dwords);
-    mcrc::build_lds_image_k1(img_k1.data(), kFixedCH);
+    mcrc::build_lds_image_k1(img_k1.data(), mcrc_dev::kK1CH);
     HIP_OK(hipMalloc(&d.img_k1, img_k1.size() * 4));
     HIP_OK(hipMemcpy(d.img_k1, img_k1.data(), img_k1.size() * 4, hipMemcpyHostToDevice));
     // rows k (k < 256) and 256 + j (x^(8 * kSegBytes * 256 j)) for every
@@ -226,11 +250,9 @@ int init_device(Device &d, int id) {
         HIP_OK(hipEventCreateWithFlags(&d.copied[k], hipEventDisableTiming));
         HIP_OK(hipEventCreateWithFlags(&d.done[k], hipEventDisableTiming));
     }
-    HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL(false), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               mcrc_dev::kLdsImageK1Bytes));
-    HIP_OK(hipFuncSetAttribute((const void *)K1_KERNEL(true), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               mcrc_dev::kLdsImageK1Bytes));
-    const void *spans[] = {
+    const void *k160[] = {
+        (const void *)mcrc_dev::k_fixed<false>,
+        (const void *)mcrc_dev::k_fixed<true>,
         (const void *)mcrc_dev::k_spans<false>,
         (const void *)mcrc_dev::k_spans<true>,
         (const void *)mcrc_dev::k_small<0>,
@@ -240,10 +262,18 @@ int init_device(Device &d, int id) {
         (const void *)mcrc_dev::k_blocks<true, true>,
         (const void *)mcrc_dev::k_blocks<true, false>,
     };
-    for (const void *k : spans)
+    for (const void *k : k160)
         HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImageK1Bytes));
     d.ok = true;
     return CRC32C_OK;
+}
+
+int ensure_devices() {  // (call with g_dev_mu held)
+    if (g_ndev < 0) {
+        g_ndev = count_gfx950();
+        for (int i = 0; i < g_ndev; ++i) g_devs.emplace_back(new Device());
+    }
+    return g_ndev;
 }
 
 // Device state for the calling thread's current HIP device.
@@ -251,10 +281,7 @@ int current_device(Device **out) {
     int id = 0;
     if (hipGetDevice(&id) != hipSuccess) return CRC32C_ENODEV;
     std::lock_guard<std::mutex> lk(g_dev_mu);
-    if (g_ndev < 0) {
-        g_ndev = count_gfx950();
-        for (int i = 0; i < g_ndev; ++i) g_devs.emplace_back(new Device());
-    }
+    ensure_devices();
     if (id < 0 || id >= g_ndev) return CRC32C_ENODEV;
     Device &d = *g_devs[id];
     if (!d.ok) {
@@ -325,23 +352,36 @@ bool one_block_len(uint32_t len) {
     return true;
 }
 
-// Batches of at most this many spans take the single-launch k_small.
-// MCRC_SMALL_MAX in the environment overrides it (read per call; the parity
-// tests run every case through both paths with 0 and the default).
+// Batches of at most g_small_max spans take the single-launch k_small
+// (crc32c_set_small_max changes it; the parity tests run every case through
+// both paths).
 constexpr uint64_t kSmallSpanMax = 1 << 20;   // fixed-length batches: spans up to 1 MiB
 constexpr uint64_t kSmallBaseMax = 8ull << 20;  // else: a buffer of at most 8 MiB (a wbuf, an IO batch)
-uint64_t small_max() {
-    const char *e = getenv("MCRC_SMALL_MAX");
-    return e ? std::min<uint64_t>(strtoull(e, nullptr, 10), mcrc_dev::kSmallMax) : mcrc_dev::kSmallMax;
-}
+std::atomic<uint64_t> g_small_max{mcrc_dev::kSmallMax};
 
 // One launch (k_small) for small batches whose spans are bounded: a group
 // reads its whole span alone, so a batch of a few multi-MiB spans is left to
-// the planned path (segments over the whole grid).
+// the planned path (segments over the whole grid).  Decided once per call.
 template <int MODE>
 bool takes_small(const mcrc_dev::SpanArgs &a) {
     const bool bounded = MODE == 0 && a.lens == nullptr ? a.len <= kSmallSpanMax : a.base_bytes <= kSmallBaseMax;
-    return a.n <= small_max() && bounded;
+    return a.n <= g_small_max.load(std::memory_order_relaxed) && bounded;
+}
+
+// k_small over a's spans on st.  Spans per workgroup: enough workgroups to
+// reach every CU (one fits a CU: 160 KiB of tables), at least 8 so that each
+// workgroup's table copy stays a few round trips (2-32 measured,
+// DESIGN.md section 3).  host_counted: a.nbad / host_nbad / done are k_small's
+// own counters and the count arrives in *host_nbad.
+template <int MODE>
+int launch_small(const Device &d, const mcrc_dev::SpanArgs &a, hipStream_t st) {
+    const uint64_t n = a.n;
+    uint64_t per = (n + d.cus - 1) / std::max(d.cus, 1);
+    per = std::min<uint64_t>(32, std::max<uint64_t>(8, (per + 1) & ~1ull));
+    hipLaunchKernelGGL((mcrc_dev::k_small<MODE>), dim3((unsigned)((n + per - 1) / per)), dim3((unsigned)(32 * per)),
+                       mcrc_dev::kLdsImageK1Bytes, st, a, d.img);
+    HIP_OK(hipGetLastError());
+    return CRC32C_OK;
 }
 
 // Unit capacity of a planned batch: units fit whenever the spans do not
@@ -351,14 +391,21 @@ uint64_t plan_cap(const mcrc_dev::SpanArgs &a) {
     return std::min<uint64_t>(a.n + a.base_bytes / mcrc_dev::kSegBytes + 1 + a.n / 4096, 0xfffffff0ull);
 }
 
-// counted: the plan entries of k_count (unit counts, item records, one-block
-// flags, zeroed accumulators) are already written (the page walk's second pass).
+// How a batch runs, decided once by the caller:
+//   small:        one k_small launch (takes_small);
+//   host_counted: (small only) k_small counts into d.small_nbad and its last
+//                 workgroup hands the count to the pinned word d.hbad (no
+//                 memset, no copy); else the caller zeroes and reads d.nbad;
+//   counted:      the plan entries of k_count are already written (the page
+//                 walk's second pass).
+struct Path {
+    bool small = false, host_counted = false, counted = false;
+};
+
 template <int MODE>
-int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st, bool counted = false,
-                 bool *host_counted = nullptr) {
+int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     const uint64_t n = a.n;
     const bool identity = MODE == 0 && a.lens == nullptr && a.len <= mcrc_dev::kSegBytes;
-    (void)aligned;
     auto spans = [&](const mcrc_dev::SpanArgs &x, int grid) {
         if (x.units)
             hipLaunchKernelGGL((mcrc_dev::k_spans<true>), dim3(grid), dim3(mcrc_dev::kSpanBlock),
@@ -372,23 +419,13 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st, 
     // groups cost 30 us of same-address atomics per 4.8 M verified items, 64 Ki
     // groups 190 us); k_count: 4096 (1024 measured 25 % slower on config 3).
     const int gf = (int)std::min<uint64_t>((n + 255) / 256, 1024);
-    if (!counted && takes_small<MODE>(a)) {
-        if (host_counted) {  // the count arrives in d.hbad (k_small's last workgroup)
+    if (path.small) {
+        if (path.host_counted) {
             a.nbad = d.small_nbad;
             a.host_nbad = d.hbad;
             a.done = d.small_done;
-            *host_counted = true;
         }
-        // spans per workgroup: enough workgroups to reach every CU (one fits a
-        // CU: 160 KiB of tables), at least 8 so that each workgroup's table
-        // copy stays a few round trips; MCRC_SMALL_SPANS overrides (dev A/B)
-        const char *e = getenv("MCRC_SMALL_SPANS");
-        uint64_t per = e ? strtoull(e, nullptr, 10) : (n + d.cus - 1) / std::max(d.cus, 1);
-        per = std::min<uint64_t>(32, std::max<uint64_t>(e ? 2 : 8, (per + 1) & ~1ull));
-        hipLaunchKernelGGL((mcrc_dev::k_small<MODE>), dim3((unsigned)((n + per - 1) / per)), dim3((unsigned)(32 * per)),
-                           mcrc_dev::kLdsImageK1Bytes, st, a, d.img);
-        HIP_OK(hipGetLastError());
-        return CRC32C_OK;
+        return launch_small<MODE>(d, a, st);
     }
     if (identity) {
         // (spans of at most kWholeMax - 15 bytes are all their threads' in k_final)
@@ -416,7 +453,7 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, bool aligned, hipStream_t st, 
     HIP_OK(hipMemsetAsync(nvalid, 0xff, 4, st));
     HIP_OK(hipMemsetAsync(nwhole, 0, 8, st));  // nwhole, nbig
     a.span_acc = d.span_acc;
-    if (!counted)
+    if (!path.counted)
         hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nunit, d.irec, d.fast);
     size_t tmp = d.scan_tmp_bytes;
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(d.scan_tmp, tmp, d.nunit, d.prefix, (int)n, st));
@@ -457,26 +494,7 @@ bool fixed_spans_fit(const crc32c_spans &s) {
     return (s.n - 1) <= (s.base_bytes - s.len) / s.stride;
 }
 
-// host_counted (synchronous callers only): a small batch's out-of-range count
-// comes back in d.hbad from k_small itself (no memset, no copy).
-int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t st, bool *host_counted = nullptr) {
-    if (s.n == 0) return CRC32C_OK;
-    if (!fixed_spans_fit(s)) return CRC32C_EINVAL;
-    const bool fixed = s.offsets == nullptr && s.lens == nullptr;
-    // every span has the same length whenever lens is absent (with or without offsets)
-    const uint32_t kspan = s.lens == nullptr ? mcrc::xpow8n(s.len) : 0u;
-    // (the lane offset within a step, item * stride, is 32-bit in K1)
-    if (fixed && s.len == kFixedLen && aligned16(s.base) && (s.stride & 15u) == 0 && s.stride < (1ull << 31)) {
-        const uint32_t kfinal = ~mcrc::Gf2Op::zeros(s.len).apply(0xffffffffu);
-        if (s.crc_in)
-            hipLaunchKernelGGL((K1_KERNEL(true)), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
-                               st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1, kfinal, kspan, s.crc_in, s.out);
-        else
-            hipLaunchKernelGGL((K1_KERNEL(false)), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
-                               st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1, kfinal, kspan, s.crc_in, s.out);
-        HIP_OK(hipGetLastError());
-    return CRC32C_OK;
-    }
+mcrc_dev::SpanArgs span_args(const Device &d, const crc32c_spans &s) {
     mcrc_dev::SpanArgs a{};
     a.base = (const uint8_t *)s.base;
     a.base_bytes = s.base_bytes;
@@ -492,11 +510,39 @@ int enqueue_device(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t
     a.xpow = d.xpow;
     a.tab8 = d.tab8;
     a.zero = d.zero;
-    const bool small = host_counted && takes_small<0>(a);
-    if (!small) HIP_OK(hipMemsetAsync(d.nbad, 0, sizeof(unsigned long long), st));
-    const bool aligned = (flags & CRC32C_ALIGNED16) ||
-                         (fixed && aligned16(s.base) && (s.stride & 15u) == 0 && (s.len & 15u) == 0);
-    return launch_units<0>(d, a, aligned, st, false, small ? host_counted : nullptr);
+    a.cfl = 4;
+    return a;
+}
+
+// want_host_count (synchronous callers only): a small batch's out-of-range
+// count comes back in d.hbad from k_small itself (no memset, no copy);
+// *host_counted says whether that happened.
+int enqueue_device(Device &d, const crc32c_spans &s, hipStream_t st, bool want_host_count = false,
+                   bool *host_counted = nullptr) {
+    if (host_counted) *host_counted = false;
+    if (s.n == 0) return CRC32C_OK;
+    if (!fixed_spans_fit(s)) return CRC32C_EINVAL;
+    const bool fixed = s.offsets == nullptr && s.lens == nullptr;
+    // (the lane offset within a step, item * stride, is 32-bit in K1)
+    if (fixed && s.len == kFixedLen && aligned16(s.base) && (s.stride & 15u) == 0 && s.stride < (1ull << 31)) {
+        if (s.crc_in)
+            hipLaunchKernelGGL((mcrc_dev::k_fixed<true>), dim3(grid_for(d, s.n)), dim3(kBlock),
+                               mcrc_dev::kLdsImageK1Bytes, st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1,
+                               s.crc_in, s.out);
+        else
+            hipLaunchKernelGGL((mcrc_dev::k_fixed<false>), dim3(grid_for(d, s.n)), dim3(kBlock),
+                               mcrc_dev::kLdsImageK1Bytes, st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1,
+                               s.crc_in, s.out);
+        HIP_OK(hipGetLastError());
+        return CRC32C_OK;
+    }
+    const mcrc_dev::SpanArgs a = span_args(d, s);
+    Path path;
+    path.small = takes_small<0>(a);
+    path.host_counted = path.small && want_host_count;
+    if (!path.host_counted) HIP_OK(hipMemsetAsync(d.nbad, 0, sizeof(unsigned long long), st));
+    if (host_counted) *host_counted = path.host_counted;
+    return launch_units<0>(d, a, st, path);
 }
 
 // [p, p + bytes) lies inside one device allocation (so no kernel read bounded
@@ -520,6 +566,24 @@ bool is_pinned_or_device(const void *p) {
         return false;
     }
     return at.type == hipMemoryTypeHost || at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+// The address a kernel reads host memory p at, when p is page-locked and
+// mapped (crc32c_host_alloc, hipHostMalloc, crc32c_host_register); nullptr for
+// pageable memory.
+const uint8_t *device_view(const void *p) {
+    hipPointerAttribute_t at;
+    if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (at.type != hipMemoryTypeHost) return nullptr;
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, const_cast<void *>(p), 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return (const uint8_t *)dp;
 }
 
 uint64_t span_off(const crc32c_spans &s, uint64_t i) { return s.offsets ? s.offsets[i] : i * s.stride; }
@@ -563,6 +627,15 @@ int ensure_slots(Device &d, uint64_t bytes, uint64_t items) {
 constexpr uint64_t kSlotBytes = 256ull << 20;  // bytes of span data per pipeline stage
 constexpr uint64_t kSlotItems = 1ull << 20;
 
+// Host spans must lie in [base, base + base_bytes) and fit a pipeline slot.
+bool host_spans_ok(const crc32c_spans &s) {
+    for (uint64_t i = 0; i < s.n; ++i) {
+        const uint64_t off = span_off(s, i), len = span_len(s, i);
+        if (off > s.base_bytes || len > s.base_bytes - off || len > kSlotBytes - 16) return false;
+    }
+    return true;
+}
+
 // Host-resident batch on one device.  Spans are staged in offset order (a
 // permutation when the caller's order is not sorted: chunked-item iov lists
 // keep their chain order) in chunks that go through two pipeline slots: while
@@ -574,10 +647,7 @@ int run_host_batch(Device &d, const crc32c_spans &s) {
     std::lock_guard<std::mutex> lk(d.mu);
     HIP_OK(hipSetDevice(d.id));
     if (s.n == 0) return CRC32C_OK;
-    for (uint64_t i = 0; i < s.n; ++i) {
-        const uint64_t off = span_off(s, i), len = span_len(s, i);
-        if (off > s.base_bytes || len > s.base_bytes - off || len > kSlotBytes - 16) return CRC32C_EINVAL;
-    }
+    if (!host_spans_ok(s)) return CRC32C_EINVAL;
     std::vector<uint64_t> order;  // staging order -> caller index (empty: identity)
     for (uint64_t i = 1; i < s.n; ++i)
         if (span_off(s, i) < span_off(s, i - 1)) {
@@ -653,7 +723,7 @@ int run_host_batch(Device &d, const crc32c_spans &s) {
         sub.crc_in = s.crc_in ? d.dcin[slot] : nullptr;
         sub.out = d.dout[slot];
         sub.n = cnt;
-        if ((rc = enqueue_device(d, sub, 0, d.stream))) return rc;
+        if ((rc = enqueue_device(d, sub, d.stream))) return rc;
         HIP_OK(hipMemcpyAsync(d.hout[slot], d.dout[slot], cnt * 4, hipMemcpyDeviceToHost, d.stream));
         HIP_OK(hipEventRecord(d.done[slot], d.stream));
         pend_k0[slot] = k0;
@@ -665,10 +735,49 @@ int run_host_batch(Device &d, const crc32c_spans &s) {
     return CRC32C_OK;
 }
 
+// Synchronous device batch on `st` (the body of crc32c_batch for
+// CRC32C_DEVICE): records the kernel time; ERANGE when a span lay outside the
+// buffer.
+int device_batch(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t st) {
+    if (s.n && !device_range_ok(s.base, s.base_bytes)) return CRC32C_EINVAL;
+    std::lock_guard<std::mutex> lk(d.mu);
+    const bool timed = !(flags & CRC32C_ASYNC);
+    d.acquire(st);
+    if (timed) HIP_OK(hipEventRecord(d.ev0, st));
+    bool host_counted = false;
+    int rc = enqueue_device(d, s, st, timed, &host_counted);
+    if (rc) {
+        d.release(st);
+        return rc;
+    }
+    if (!timed) {
+        d.release(st);
+        return CRC32C_OK;
+    }
+    HIP_OK(hipEventRecord(d.ev1, st));
+    // spans given by offsets / lengths are range-checked on the device
+    unsigned long long nrange = 0;
+    const bool checked = s.n && (s.offsets || s.lens);
+    if (checked && !host_counted) HIP_OK(hipMemcpyAsync(d.hbad, d.nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
+    d.release(st);
+    HIP_OK(hipEventSynchronize(d.ev1));
+    if (checked) {
+        HIP_OK(hipStreamSynchronize(st));
+        nrange = *d.hbad;
+    }
+    (void)hipEventElapsedTime(&g_last_kernel_ms, d.ev0, d.ev1);
+    return nrange ? CRC32C_ERANGE : CRC32C_OK;
+}
+
 // Item-image batches (verify: MODE 1, stamp: MODE 2) over a packed buffer of
-// item images at item_offsets.  Host buffers are staged through device memory;
-// stamp on a host buffer brings back only the CRCs and writes them into the
-// images' exptime fields here.
+// item images at item_offsets.
+//   device: in place on the caller's stream;
+//   host, small (at most 8 MiB, a wbuf or an IO batch): one k_small launch on
+//     the library stream that reads the images where they are when the buffer
+//     is page-locked (crc32c_host_alloc / _register; stamps are written into
+//     it in place), else from a pinned copy; descriptors and results through
+//     pinned mapped scratch -- no device allocation, no copy engine;
+//   host, large: staged into grow-only device scratch, planned kernels.
 template <int MODE>
 int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const uint64_t *item_offsets, uint64_t n,
                 uint8_t *ok, uint64_t *nbad, unsigned flags, void *stream) {
@@ -680,86 +789,302 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
         if (nbad) *nbad = 0;
         return CRC32C_OK;
     }
-    hipStream_t st = (hipStream_t)stream;  // NULL: the default stream
     const bool dev = flags & CRC32C_DEVICE;
     if (dev && !device_range_ok(base, base_bytes)) return CRC32C_EINVAL;
-    std::lock_guard<std::mutex> lk(d->mu);
-    const uint8_t *dbase = (const uint8_t *)base;
-    const uint64_t *doffs = item_offsets;
-    uint8_t *dok = ok;
-    uint32_t *dcrc = nullptr;
-    std::vector<void *> tmp;
-    auto dalloc = [&](size_t bytes) -> void * {
-        void *p = nullptr;
-        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-        tmp.push_back(p);
-        return p;
-    };
-    auto cleanup = [&]() {
-        for (void *p : tmp) (void)hipFree(p);
-    };
-    if (!dev) {
-        uint8_t *b = (uint8_t *)dalloc(base_bytes);
-        uint64_t *o = (uint64_t *)dalloc(n * 8);
-        dok = (uint8_t *)dalloc(n);
-        if (MODE == 2) dcrc = (uint32_t *)dalloc(n * 4);
-        if (!b || !o || !dok || (MODE == 2 && !dcrc)) {
-            cleanup();
-            return CRC32C_ENOMEM;
-        }
-        if (hipMemcpyAsync(b, base, base_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
-            hipMemcpyAsync(o, item_offsets, n * 8, hipMemcpyHostToDevice, st) != hipSuccess) {
-            cleanup();
-            return CRC32C_EHIP;
-        }
-        dbase = b;
-        doffs = o;
-    }
     mcrc_dev::SpanArgs a{};
-    a.base = dbase;
+    a.base = (const uint8_t *)base;
     a.base_bytes = base_bytes;
-    a.offsets = doffs;
-    a.ok = dok;
-    a.out = dcrc;  // stamp: nullptr = write into the images
+    a.offsets = item_offsets;
     a.nbad = d->nbad;
     a.n = n;
     a.xpow = d->xpow;
     a.tab8 = d->tab8;
     a.zero = d->zero;
     a.region = region_bytes;
+    a.cfl = (flags & CRC32C_CFLAGS64) ? 8u : 4u;
+    Path path;
+    path.small = takes_small<MODE>(a);
+    std::lock_guard<std::mutex> lk(d->mu);
+    if (dev) {
+        hipStream_t st = (hipStream_t)stream;  // NULL: the default stream
+        a.ok = ok;
+        a.out = nullptr;  // stamp: write into the images
+        path.host_counted = path.small;
+        d->acquire(st);
+        if (!path.host_counted) (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
+        rc = launch_units<MODE>(*d, a, st, path);
+        if (!rc && !path.host_counted)
+            rc = hipMemcpyAsync(d->hbad, d->nbad, sizeof(unsigned long long), hipMemcpyDeviceToHost, st) == hipSuccess
+                     ? CRC32C_OK
+                     : CRC32C_EHIP;
+        d->release(st);
+        if (rc) return rc;
+        if ((flags & CRC32C_ASYNC) && !nbad) return CRC32C_OK;  // fire and forget
+        HIP_OK(hipStreamSynchronize(st));
+        if (nbad) *nbad = *d->hbad;
+        return CRC32C_OK;
+    }
+    hipStream_t st = d->stream;
+    HIP_OK(hipSetDevice(d->id));
     d->acquire(st);
-    const bool small = takes_small<MODE>(a);  // (then the count comes back in d->hbad)
-    if (!small) (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
-    bool host_counted = false;
-    rc = launch_units<MODE>(*d, a, false, st, false, &host_counted);
-    d->release(st);
-    if (rc) {
-        cleanup();
-        return rc;
+    struct Release {
+        Device *d;
+        hipStream_t st;
+        ~Release() {
+            (void)hipStreamSynchronize(st);
+            d->release(st);
+        }
+    } release_on_exit{d, st};
+    void *h_offs, *v_offs, *h_ok, *v_ok, *h_crc = nullptr, *v_crc = nullptr;
+    if (!d->grow_pinned(kPinOffs, n * 8, &h_offs, &v_offs) || !d->grow_pinned(kPinOk, n, &h_ok, &v_ok))
+        return CRC32C_ENOMEM;
+    memcpy(h_offs, item_offsets, n * 8);
+    const uint8_t *mapped = device_view(base);
+    // stamp results come back as CRCs (scattered into the caller's images
+    // here) unless the kernel stamps the caller's page-locked buffer itself
+    const bool crcs_back = MODE == 2 && !(path.small && mapped);
+    if (crcs_back && !d->grow_pinned(kPinCrc, n * 4, &h_crc, &v_crc)) return CRC32C_ENOMEM;
+    a.ok = (uint8_t *)v_ok;
+    a.out = (uint32_t *)v_crc;
+    if (path.small) {
+        if (!mapped) {  // a pinned copy the kernel reads
+            void *h_stage, *v_stage;
+            if (!d->grow_pinned(kPinStage, base_bytes, &h_stage, &v_stage)) return CRC32C_ENOMEM;
+            memcpy(h_stage, base, base_bytes);
+            mapped = (const uint8_t *)v_stage;
+        }
+        a.base = mapped;
+        a.offsets = (const uint64_t *)v_offs;
+        path.host_counted = true;
+        if ((rc = launch_units<MODE>(*d, a, st, path))) return rc;
+    } else {
+        uint8_t *b = (uint8_t *)d->grow(kScrStage, base_bytes);
+        uint64_t *o = (uint64_t *)d->grow(kScrItemOffs, n * 8);
+        uint8_t *r = (uint8_t *)d->grow(kScrItemOut, n * 5 + 4);  // ok[n], then (4-B aligned) crc[n]
+        if (!b || !o || !r) return CRC32C_ENOMEM;
+        HIP_OK(hipMemcpyAsync(b, base, base_bytes, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(o, h_offs, n * 8, hipMemcpyHostToDevice, st));
+        a.base = b;
+        a.offsets = o;
+        a.ok = r;
+        a.out = crcs_back ? (uint32_t *)(r + ((n + 3) & ~3ull)) : nullptr;
+        HIP_OK(hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st));
+        if ((rc = launch_units<MODE>(*d, a, st, path))) return rc;
+        HIP_OK(hipMemcpyAsync(h_ok, a.ok, n, hipMemcpyDeviceToHost, st));
+        if (crcs_back) HIP_OK(hipMemcpyAsync(h_crc, a.out, n * 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     }
-    if (dev && (flags & CRC32C_ASYNC) && !nbad) return CRC32C_OK;  // device, fire and forget
-    unsigned long long bad = 0;
-    std::vector<uint32_t> crcs;
-    std::vector<uint8_t> oks;
-    bool fail = !host_counted && hipMemcpyAsync(d->hbad, d->nbad, sizeof bad, hipMemcpyDeviceToHost, st) != hipSuccess;
-    if (!dev && MODE == 1) fail = fail || hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, st) != hipSuccess;
-    if (!dev && MODE == 2) {
-        crcs.resize(n);
-        oks.resize(n);
-        fail = fail || hipMemcpyAsync(crcs.data(), dcrc, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-               hipMemcpyAsync(oks.data(), dok, n, hipMemcpyDeviceToHost, st) != hipSuccess;
-    }
-    fail = fail || hipStreamSynchronize(st) != hipSuccess;
-    cleanup();
-    if (fail) return CRC32C_EHIP;
-    bad = *d->hbad;
-    if (!dev && MODE == 2) {
-        uint8_t *b = (uint8_t *)base;
+    HIP_OK(hipStreamSynchronize(st));
+    const uint8_t *oks = (const uint8_t *)h_ok;
+    if (crcs_back) {
+        uint8_t *bb = (uint8_t *)base;
+        const uint32_t *crcs = (const uint32_t *)h_crc;
         for (uint64_t i = 0; i < n; ++i)
-            if (oks[i]) memcpy(b + item_offsets[i] + 28, &crcs[i], 4);  // exptime (storage.c:567)
-        if (ok) memcpy(ok, oks.data(), n);
+            if (oks[i]) memcpy(bb + item_offsets[i] + 28, &crcs[i], 4);  // exptime (storage.c:567)
     }
-    if (nbad) *nbad = bad;
+    if (ok) memcpy(ok, oks, n);
+    if (nbad) *nbad = *d->hbad;
+    return CRC32C_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Coalescing queue (crc32c_batch_submit / _wait)
+// ---------------------------------------------------------------------------
+// The read-verify CRCs arrive from many IO threads, each with a batch of at
+// most io_depth reads (extstore.c:853-945; io_depth = 1 by default,
+// storage.c:1339).  One synchronous GPU call per such batch costs a launch and
+// a round trip per thread; the queue instead lets every thread enqueue its
+// spans and a per-device dispatcher packs whatever is pending into one k_small
+// launch, reading the spans where they lie in page-locked host memory
+// (group commit: while one launch runs, the next batch accumulates).
+struct crc32c_job {
+    crc32c_spans s;
+    unsigned flags = 0;
+    const uint8_t *dbase = nullptr;  // coalesced jobs: the device view of s.base
+    bool coalesce = false;
+    int rc = CRC32C_OK;
+    std::atomic<int> done{0};
+    Queue *q = nullptr;
+};
+
+namespace {
+
+constexpr uint64_t kQueueSpanMax = 256u << 10;  // longer spans: the job runs alone (planned path)
+
+struct Queue {
+    Device *d = nullptr;
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    std::deque<crc32c_job *> pending;
+    hipStream_t st = nullptr;
+    // pinned, mapped descriptors of one launch (kSmallMax spans each)
+    uint64_t *addr = nullptr;
+    uint32_t *len = nullptr, *cin = nullptr, *out = nullptr;
+    void *v_addr = nullptr, *v_len = nullptr, *v_cin = nullptr, *v_out = nullptr;
+    unsigned long long *dnbad = nullptr;  // (spans are absolute: never out of range)
+    std::atomic<uint64_t> launches{0}, spans{0}, jobs{0}, solo{0};
+
+    int init(Device &dev) {
+        d = &dev;
+        HIP_OK(hipSetDevice(dev.id));
+        HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        const uint64_t n = mcrc_dev::kSmallMax;
+        HIP_OK(hipHostMalloc((void **)&addr, n * 8, hipHostMallocDefault));
+        HIP_OK(hipHostMalloc((void **)&len, n * 4, hipHostMallocDefault));
+        HIP_OK(hipHostMalloc((void **)&cin, n * 4, hipHostMallocDefault));
+        HIP_OK(hipHostMalloc((void **)&out, n * 4, hipHostMallocDefault));
+        HIP_OK(hipHostGetDevicePointer(&v_addr, addr, 0));
+        HIP_OK(hipHostGetDevicePointer(&v_len, len, 0));
+        HIP_OK(hipHostGetDevicePointer(&v_cin, cin, 0));
+        HIP_OK(hipHostGetDevicePointer(&v_out, out, 0));
+        HIP_OK(hipMalloc(&dnbad, sizeof(unsigned long long)));
+        HIP_OK(hipMemset(dnbad, 0, sizeof(unsigned long long)));
+        // the dispatcher lives as long as the process (never joined: the queue
+        // is not freed, and at exit the thread is blocked on cv_work)
+        std::thread([this] { run(); }).detach();
+        return CRC32C_OK;
+    }
+
+    void submit(crc32c_job *j) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            pending.push_back(j);
+        }
+        cv_work.notify_one();
+    }
+
+    void complete(crc32c_job *j, int rc) {
+        j->rc = rc;
+        {
+            std::lock_guard<std::mutex> lk(mu);  // (no lost wake-up between a waiter's check and wait)
+            j->done.store(1, std::memory_order_release);
+        }
+        cv_done.notify_all();
+    }
+
+    int wait(crc32c_job *j) {
+        // completions come within tens of microseconds: spin a little first
+        for (int i = 0; i < 4096 && !j->done.load(std::memory_order_acquire); ++i) std::this_thread::yield();
+        if (!j->done.load(std::memory_order_acquire)) {
+            std::unique_lock<std::mutex> lk(mu);
+            cv_done.wait(lk, [&] { return j->done.load(std::memory_order_acquire) != 0; });
+        }
+        return j->rc;
+    }
+
+    // Every job of `batch` in one k_small launch over absolute span addresses.
+    int launch(const std::vector<crc32c_job *> &batch) {
+        uint64_t k = 0;
+        for (crc32c_job *j : batch) {
+            const crc32c_spans &s = j->s;
+            for (uint64_t i = 0; i < s.n; ++i, ++k) {
+                addr[k] = (uint64_t)(uintptr_t)(j->dbase + span_off(s, i));
+                len[k] = (uint32_t)span_len(s, i);
+                cin[k] = s.crc_in ? s.crc_in[i] : 0u;
+            }
+        }
+        mcrc_dev::SpanArgs a{};
+        a.base = nullptr;  // spans at absolute addresses
+        a.base_bytes = ~0ull;
+        a.offsets = (const uint64_t *)v_addr;
+        a.lens = (const uint32_t *)v_len;
+        a.crc_in = (const uint32_t *)v_cin;
+        a.out = (uint32_t *)v_out;
+        a.nbad = dnbad;
+        a.n = k;
+        a.xpow = d->xpow;
+        a.tab8 = d->tab8;
+        a.zero = d->zero;
+        a.cfl = 4;
+        int rc = launch_small<0>(*d, a, st);
+        if (rc) return rc;
+        HIP_OK(hipStreamSynchronize(st));
+        k = 0;
+        for (crc32c_job *j : batch) {
+            memcpy(j->s.out, out + k, j->s.n * 4);
+            k += j->s.n;
+        }
+        launches.fetch_add(1, std::memory_order_relaxed);
+        spans.fetch_add(k, std::memory_order_relaxed);
+        jobs.fetch_add(batch.size(), std::memory_order_relaxed);
+        return CRC32C_OK;
+    }
+
+    int run_solo(crc32c_job *j) {
+        solo.fetch_add(1, std::memory_order_relaxed);
+        if (j->flags & CRC32C_DEVICE) return device_batch(*d, j->s, j->flags & ~(unsigned)CRC32C_ASYNC, st);
+        return run_host_batch(*d, j->s);
+    }
+
+    void run() {
+        (void)hipSetDevice(d->id);
+        std::vector<crc32c_job *> batch;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv_work.wait(lk, [&] { return !pending.empty(); });
+                batch.clear();
+                if (!pending.front()->coalesce) {
+                    batch.push_back(pending.front());
+                    pending.pop_front();
+                } else {
+                    uint64_t ns = 0;
+                    while (!pending.empty() && pending.front()->coalesce &&
+                           ns + pending.front()->s.n <= mcrc_dev::kSmallMax) {
+                        ns += pending.front()->s.n;
+                        batch.push_back(pending.front());
+                        pending.pop_front();
+                    }
+                }
+            }
+            if (!batch[0]->coalesce) {
+                complete(batch[0], run_solo(batch[0]));
+                continue;
+            }
+            const int rc = launch(batch);
+            for (crc32c_job *j : batch) complete(j, rc);
+        }
+    }
+};
+
+int queue_of(Device &d, Queue **out) {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!d.queue) {
+        Queue *q = new Queue();
+        const int rc = q->init(d);
+        if (rc) return rc;  // (a partly initialised queue is leaked, not reused)
+        d.queue = q;
+    }
+    *out = d.queue;
+    return CRC32C_OK;
+}
+
+// A new job for the current device's queue; *coalesce says whether it can
+// share a launch (host spans, device-visible buffer, short spans).
+int make_job(const crc32c_spans &s, unsigned flags, crc32c_job **out) {
+    if (s.n && (!s.base || !s.out)) return CRC32C_EINVAL;
+    Device *d = nullptr;
+    int rc = current_device(&d);
+    if (rc) return rc;
+    Queue *q = nullptr;
+    if ((rc = queue_of(*d, &q))) return rc;
+    crc32c_job *j = new crc32c_job();
+    j->s = s;
+    j->flags = flags & ~(unsigned)CRC32C_ASYNC;
+    j->q = q;
+    if (!(flags & CRC32C_DEVICE)) {
+        if (!host_spans_ok(s)) {
+            delete j;
+            return CRC32C_EINVAL;
+        }
+        bool short_spans = s.n >= 1 && s.n <= mcrc_dev::kSmallMax;
+        for (uint64_t i = 0; short_spans && i < s.n; ++i) short_spans = span_len(s, i) <= kQueueSpanMax;
+        if (short_spans && (j->dbase = device_view(s.base)) != nullptr) j->coalesce = true;
+    }
+    *out = j;
     return CRC32C_OK;
 }
 
@@ -772,11 +1097,7 @@ extern "C" {
 
 int crc32c_gpu_count(void) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
-    if (g_ndev < 0) {
-        g_ndev = count_gfx950();
-        for (int i = 0; i < g_ndev; ++i) g_devs.emplace_back(new Device());
-    }
-    return g_ndev;
+    return ensure_devices();
 }
 
 void *crc32c_host_alloc(size_t bytes) {
@@ -789,6 +1110,24 @@ void *crc32c_host_alloc(size_t bytes) {
 
 void crc32c_host_free(void *p) {
     if (p) (void)hipHostFree(p);
+}
+
+int crc32c_host_register(void *p, size_t bytes) {
+    if (!p || !bytes) return CRC32C_EINVAL;
+    if (crc32c_gpu_count() <= 0) return CRC32C_ENODEV;
+    HIP_OK(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    return CRC32C_OK;
+}
+
+int crc32c_host_unregister(void *p) {
+    if (!p) return CRC32C_EINVAL;
+    if (crc32c_gpu_count() <= 0) return CRC32C_ENODEV;
+    HIP_OK(hipHostUnregister(p));
+    return CRC32C_OK;
+}
+
+uint64_t crc32c_set_small_max(uint64_t n) {
+    return g_small_max.exchange(std::min<uint64_t>(n, mcrc_dev::kSmallMax));
 }
 
 const char *crc32c_strerror(int err) {
@@ -805,43 +1144,57 @@ const char *crc32c_strerror(int err) {
 
 float crc32c_last_kernel_ms(void) { return g_last_kernel_ms; }
 
+int crc32c_batch_submit(const crc32c_spans *s, unsigned flags, crc32c_job_t *job) {
+    if (!s || !job) return CRC32C_EINVAL;
+    crc32c_job *j = nullptr;
+    const int rc = make_job(*s, flags, &j);
+    if (rc) return rc;
+    j->q->submit(j);
+    *job = j;
+    return CRC32C_OK;
+}
+
+int crc32c_batch_wait(crc32c_job_t j) {
+    if (!j) return CRC32C_EINVAL;
+    const int rc = j->q->wait(j);
+    delete j;
+    return rc;
+}
+
+int crc32c_queue_stats(uint64_t *launches, uint64_t *spans, uint64_t *jobs, uint64_t *solo_jobs) {
+    Device *d = nullptr;
+    const int rc = current_device(&d);
+    if (rc) return rc;
+    const Queue *q = d->queue;
+    if (launches) *launches = q ? q->launches.load() : 0;
+    if (spans) *spans = q ? q->spans.load() : 0;
+    if (jobs) *jobs = q ? q->jobs.load() : 0;
+    if (solo_jobs) *solo_jobs = q ? q->solo.load() : 0;
+    return CRC32C_OK;
+}
+
 int crc32c_batch(const crc32c_spans *s, unsigned flags, void *stream) {
     if (!s || (s->n && (!s->base || !s->out))) return CRC32C_EINVAL;
     Device *d = nullptr;
     int rc = current_device(&d);
     if (rc) return rc;
-    if (!(flags & CRC32C_DEVICE)) return run_host_batch(*d, *s);
-    // Device batches run on the caller's stream; NULL is the default stream, so
-    // the kernel is ordered after whatever produced the buffers there.
-    hipStream_t st = (hipStream_t)stream;
-    const bool timed = !(flags & CRC32C_ASYNC);
-    if (s->n && !device_range_ok(s->base, s->base_bytes)) return CRC32C_EINVAL;
-    std::lock_guard<std::mutex> lk(d->mu);
-    d->acquire(st);
-    if (timed) HIP_OK(hipEventRecord(d->ev0, st));
-    bool host_counted = false;
-    rc = enqueue_device(*d, *s, flags, st, timed ? &host_counted : nullptr);
-    if (rc) {
-        d->release(st);
+    if (!(flags & CRC32C_DEVICE)) {
+        // short spans in page-locked memory share the queue's launches with
+        // other threads' batches; anything else is staged on its own
+        crc32c_job *j = nullptr;
+        if ((rc = make_job(*s, flags, &j))) return rc;
+        if (!j->coalesce) {
+            delete j;
+            return run_host_batch(*d, *s);
+        }
+        j->q->submit(j);
+        rc = j->q->wait(j);
+        delete j;
         return rc;
     }
-    if (!timed) {
-        d->release(st);
-        return CRC32C_OK;
-    }
-    HIP_OK(hipEventRecord(d->ev1, st));
-    // spans given by offsets / lengths are range-checked on the device
-    unsigned long long nrange = 0;
-    const bool checked = s->n && (s->offsets || s->lens);
-    if (checked && !host_counted) HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
-    d->release(st);
-    HIP_OK(hipEventSynchronize(d->ev1));
-    if (checked) {
-        HIP_OK(hipStreamSynchronize(st));
-        nrange = *d->hbad;
-    }
-    (void)hipEventElapsedTime(&g_last_kernel_ms, d->ev0, d->ev1);
-    return nrange ? CRC32C_ERANGE : CRC32C_OK;
+    // Device batches run on the caller's stream; NULL is the default stream, so
+    // the kernel is ordered after whatever produced the buffers there.
+    return device_batch(*d, *s, flags, (hipStream_t)stream);
 }
 
 int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, uint64_t nchains, uint32_t *out,
@@ -873,7 +1226,7 @@ int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, u
     bool nrange_copied = false;
     if (dev) {
         if (!device_range_ok(iovs->base, iovs->base_bytes)) return CRC32C_EINVAL;
-        rc = enqueue_device(*d, *iovs, flags, st);
+        rc = enqueue_device(*d, *iovs, st);
         if (rc) return rc;
         if (!(flags & CRC32C_ASYNC) && (iovs->offsets || iovs->lens)) {  // range-checked on the device
             HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof nrange, hipMemcpyDeviceToHost, st));
@@ -959,6 +1312,7 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     a.tab8 = d->tab8;
     a.zero = d->zero;
     a.region = wbuf_bytes;
+    a.cfl = (flags & CRC32C_CFLAGS64) ? 8u : 4u;
     // one walking wave per wbuf, kWalkWaves per workgroup
     const int gw = (int)std::min<uint64_t>((nw + mcrc_dev::kWalkWaves - 1) / mcrc_dev::kWalkWaves, 65535);
     const dim3 bw(64 * mcrc_dev::kWalkWaves);
@@ -984,20 +1338,22 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     a.n = total;
     // the second walk writes the offsets and, for a planned verify, the plan
     // entries k_count would make (the headers are read once more, not twice)
-    const bool planned = !takes_small<1>(a);
-    if (planned) {
+    Path path;
+    path.small = takes_small<1>(a);
+    path.counted = !path.small;
+    if (path.counted) {
         rc = ensure_plan(*d, total, plan_cap(a));
         if (rc) return rc;
         a.span_acc = d->span_acc;
     }
     wo.prefix = prefix;
     wo.offs = doffs;
-    wo.nunit = planned ? d->nunit : nullptr;
-    wo.irec = planned ? d->irec : nullptr;
-    wo.fast = planned ? d->fast : nullptr;
+    wo.nunit = path.counted ? d->nunit : nullptr;
+    wo.irec = path.counted ? d->irec : nullptr;
+    wo.fast = path.counted ? d->fast : nullptr;
     hipLaunchKernelGGL(mcrc_dev::k_walk<true>, dim3(gw), bw, 0, st, a, nw, wo);
     HIP_OK(hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st));
-    rc = launch_units<1>(*d, a, false, st, /*counted=*/planned);
+    rc = launch_units<1>(*d, a, st, path);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     const uint64_t k = std::min<uint64_t>(cap, total);
@@ -1011,22 +1367,30 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     return CRC32C_OK;
 }
 
+int crc32c_shard_cuts(const uint32_t *lens, uint32_t len, uint64_t n, int parts, uint64_t *cuts) {
+    if (parts < 1 || !cuts) return CRC32C_EINVAL;
+    unsigned __int128 total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += lens ? lens[i] : len;
+    cuts[0] = 0;
+    uint64_t i = 0;
+    unsigned __int128 acc = 0;
+    for (int g = 1; g < parts; ++g) {
+        const unsigned __int128 target = total * (unsigned)g / (unsigned)parts;
+        for (; i < n && acc < target; ++i) acc += lens ? lens[i] : len;
+        cuts[g] = i;
+    }
+    cuts[parts] = n;
+    return CRC32C_OK;
+}
+
 int crc32c_batch_multi(const crc32c_spans *s, int ngpus) {
     if (!s) return CRC32C_EINVAL;
     const int avail = crc32c_gpu_count();
     if (avail <= 0) return CRC32C_ENODEV;
     if (ngpus <= 0 || ngpus > avail) ngpus = avail;
-    // split by bytes: shard g gets spans whose cumulative length falls in its share
-    uint64_t total = 0;
-    for (uint64_t i = 0; i < s->n; ++i) total += span_len(*s, i);
-    std::vector<uint64_t> cut(ngpus + 1, s->n);
-    cut[0] = 0;
-    uint64_t acc = 0, i = 0;
-    for (int g = 1; g < ngpus; ++g) {
-        const uint64_t target = total * g / ngpus;
-        while (i < s->n && acc < target) acc += span_len(*s, i++);
-        cut[g] = i;
-    }
+    std::vector<uint64_t> cut(ngpus + 1);
+    int rc = crc32c_shard_cuts(s->lens, s->len, s->n, ngpus, cut.data());
+    if (rc) return rc;
     std::vector<int> rcs(ngpus, CRC32C_OK);
     std::vector<std::thread> th;
     for (int g = 0; g < ngpus; ++g) {
@@ -1051,45 +1415,9 @@ int crc32c_batch_multi(const crc32c_spans *s, int ngpus) {
         });
     }
     for (auto &t : th) t.join();
-    for (int rc : rcs)
-        if (rc) return rc;
+    for (int r : rcs)
+        if (r) return r;
     return CRC32C_OK;
-}
-
-struct crc32c_job {
-    crc32c_spans spans;
-    unsigned flags;
-    int device;
-    std::thread worker;
-    int rc;
-};
-
-int crc32c_batch_submit(const crc32c_spans *s, unsigned flags, crc32c_job_t *job) {
-    if (!s || !job) return CRC32C_EINVAL;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return CRC32C_ENODEV;
-    crc32c_job *j = new crc32c_job();
-    j->spans = *s;
-    j->flags = flags & ~CRC32C_ASYNC;
-    j->device = dev;
-    j->rc = CRC32C_OK;
-    j->worker = std::thread([j]() {
-        if (hipSetDevice(j->device) != hipSuccess) {
-            j->rc = CRC32C_EHIP;
-            return;
-        }
-        j->rc = crc32c_batch(&j->spans, j->flags, nullptr);
-    });
-    *job = j;
-    return CRC32C_OK;
-}
-
-int crc32c_batch_wait(crc32c_job_t j) {
-    if (!j) return CRC32C_EINVAL;
-    j->worker.join();
-    const int rc = j->rc;
-    delete j;
-    return rc;
 }
 
 }  // extern "C"

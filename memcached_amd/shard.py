@@ -14,8 +14,10 @@ import numpy as np
 def plan(lens, world: int):
     """Return world+1 cut points c with rank r owning items [c[r], c[r+1]).
 
-    Rank r's range starts at the first item whose byte prefix reaches
-    total * r / world (so every rank gets about total / world bytes).
+    c[r] is the first item index i whose byte prefix sum(lens[:i]) reaches
+    total * r // world, so every rank gets about total / world bytes -- the
+    rule of crc32c_shard_cuts (include/crc32c_batch.h), which tests check
+    this function against.
     """
     lens = np.asarray(lens, dtype=np.uint64)
     n = lens.size
@@ -23,13 +25,8 @@ def plan(lens, world: int):
         raise ValueError("world must be >= 1")
     prefix = np.concatenate([[0], np.cumsum(lens, dtype=np.uint64)])
     total = int(prefix[-1])
-    cuts = [0]
-    for r in range(1, world):
-        target = total * r // world
-        cuts.append(int(np.searchsorted(prefix[1:], target, side="left")) + (1 if total else 0))
-        cuts[-1] = min(max(cuts[-1], cuts[-2]), n)
-    cuts.append(n)
-    return np.asarray(cuts, dtype=np.int64)
+    cuts = [int(np.searchsorted(prefix, np.uint64(total * r // world), side="left")) for r in range(world)]
+    return np.asarray(cuts + [n], dtype=np.int64)
 
 
 def plan_equal(n: int, world: int):

@@ -3,11 +3,14 @@
  * Linked with the reference crc32c.c (compiled in place from /root/reference by
  * oracle/Makefile into oracle/_ref/libref_crc32c.so).  Exposes the reference
  * crc32c function pointer to ctypes and a pthread timing harness used for the
- * cpu_baseline leg of bench.py: one thread per requested core, static
+ * cpu_baseline leg of bench.py: one thread per requested core (optionally
+ * pinned to a given CPU list: one logical CPU per physical core), static
  * contiguous split of the item array, each item checksummed with
  * crc32c(0, item, len) exactly as storage.c:567 does.
  */
+#define _GNU_SOURCE
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <time.h>
@@ -35,10 +38,11 @@ static void *worker(void *arg) {
     return NULL;
 }
 
-/* Checksums n items with `threads` threads; returns wall seconds. */
-double ref_crc32c_batch_timed(const unsigned char *base, const uint64_t *offsets,
-                              const uint64_t *lens, uint64_t stride, uint64_t len, uint64_t n,
-                              int threads, uint32_t *out) {
+/* Checksums n items with `threads` threads (thread t pinned to cpus[t] when
+ * cpus is not NULL); returns wall seconds. */
+double ref_crc32c_batch_timed_cpus(const unsigned char *base, const uint64_t *offsets,
+                                   const uint64_t *lens, uint64_t stride, uint64_t len, uint64_t n,
+                                   int threads, uint32_t *out, const int *cpus) {
     if (threads < 1) threads = 1;
     pthread_t *tid = calloc((size_t)threads, sizeof *tid);
     struct job *jobs = calloc((size_t)threads, sizeof *jobs);
@@ -47,11 +51,26 @@ double ref_crc32c_batch_timed(const unsigned char *base, const uint64_t *offsets
     for (int t = 0; t < threads; t++) {
         jobs[t] = (struct job){base, offsets, lens, stride, len, n * t / threads,
                                n * (t + 1) / threads, out};
-        pthread_create(&tid[t], NULL, worker, &jobs[t]);
+        pthread_attr_t attr;
+        pthread_attr_init(&attr);
+        if (cpus) {
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            CPU_SET(cpus[t], &set);
+            pthread_attr_setaffinity_np(&attr, sizeof set, &set);
+        }
+        pthread_create(&tid[t], &attr, worker, &jobs[t]);
+        pthread_attr_destroy(&attr);
     }
     for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     free(tid);
     free(jobs);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+double ref_crc32c_batch_timed(const unsigned char *base, const uint64_t *offsets,
+                              const uint64_t *lens, uint64_t stride, uint64_t len, uint64_t n,
+                              int threads, uint32_t *out) {
+    return ref_crc32c_batch_timed_cpus(base, offsets, lens, stride, len, n, threads, out, NULL);
 }

@@ -20,15 +20,14 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 @pytest.fixture(autouse=True, params=["small", "planned"])
-def span_path(request, monkeypatch):
+def span_path(request):
     """Every case runs twice: batches of at most 8192 spans through the
     single-launch k_small (the default) and through the planned path
-    (count / scan / expand / span kernel / final) that larger batches take."""
-    if request.param == "planned":
-        monkeypatch.setenv("MCRC_SMALL_MAX", "0")
-    else:
-        monkeypatch.delenv("MCRC_SMALL_MAX", raising=False)
-    return request.param
+    (count / scan / expand / span kernel / final) that larger batches take
+    (crc32c_set_small_max(0))."""
+    prev = _lib.lib.crc32c_set_small_max(0 if request.param == "planned" else 8192)
+    yield request.param
+    _lib.lib.crc32c_set_small_max(prev)
 
 
 @pytest.fixture(scope="module")

@@ -1,9 +1,15 @@
-"""The extstore CRC flow of storage.c driven through libmcrc32c.so from C
-(tests/integration/storage_sim.c): scalar drop-in on the CPU; batched spill
-stamping, page walk + verify and an IO read batch on the GPU.  BASELINE
-configs[0] (tests/integration/extstore_config1.c): 10 000 SETs of 4 KiB values
-spilled to a page file and read back, checked against the reference's CRCs of
-the same items (tests/golden/config1.json)."""
+"""The extstore CRC flow of storage.c driven through libmcrc32c.so from C:
+
+* storage_sim.c: scalar drop-in on the CPU; batched spill stamping, page walk
+  + verify and an IO read batch on the GPU.
+* extstore_config1.c: BASELINE configs[0], 10 000 SETs of 4 KiB values spilled
+  to a page file and read back, checked against the reference's CRCs of the
+  same items (tests/golden/config1.json).
+* queue_sim.c: many IO threads' read-verify batches (io_depth-sized,
+  extstore.c:853-945) through the coalescing queue.
+* extstore_sim.c: the deferred (batched) spill CRC under a concurrent writer,
+  flusher and readers, with the open-wbuf read fence -- and without it, the
+  negative control that shows the false bad CRCs the fence prevents."""
 import json
 import os
 import re
@@ -19,14 +25,18 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
 
-@pytest.fixture(scope="module")
-def sim(tmp_path_factory):
+def _build_c(tmp_path_factory, name):
     lib = build.build_lib()
-    exe = str(tmp_path_factory.mktemp("sim") / "storage_sim")
-    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(HERE, "integration", "storage_sim.c"), "-L", os.path.dirname(lib), "-lmcrc32c",
+    exe = str(tmp_path_factory.mktemp(name) / name)
+    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-pthread", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(HERE, "integration", name + ".c"), "-L", os.path.dirname(lib), "-lmcrc32c",
                     f"-Wl,-rpath,{os.path.dirname(lib)}", "-o", exe], check=True)
     return exe
+
+
+@pytest.fixture(scope="module")
+def sim(tmp_path_factory):
+    return _build_c(tmp_path_factory, "storage_sim")
 
 
 def test_storage_sim_scalar_dropin(sim):
@@ -45,12 +55,7 @@ def test_storage_sim_gpu(sim):
 
 @pytest.fixture(scope="module")
 def config1_exe(tmp_path_factory):
-    lib = build.build_lib()
-    exe = str(tmp_path_factory.mktemp("cfg1") / "extstore_config1")
-    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(HERE, "integration", "extstore_config1.c"), "-L", os.path.dirname(lib), "-lmcrc32c",
-                    f"-Wl,-rpath,{os.path.dirname(lib)}", "-o", exe], check=True)
-    return exe
+    return _build_c(tmp_path_factory, "extstore_config1")
 
 
 def _golden_config1():
@@ -100,3 +105,70 @@ def test_config1_extstore_batched_gpu(config1_exe, tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "config1 gpu: stamped == scalar, page verify nbad 0, read batch mismatches 0" in r.stdout
     assert "digest %08x" % _golden_config1()["digest"] in r.stdout
+
+
+@pytest.fixture(scope="module")
+def queue_exe(tmp_path_factory):
+    return _build_c(tmp_path_factory, "queue_sim")
+
+
+@pytest.fixture(scope="module")
+def extstore_exe(tmp_path_factory):
+    return _build_c(tmp_path_factory, "extstore_sim")
+
+
+_NOGPU = dict(os.environ, HIP_VISIBLE_DEVICES="-1")
+
+
+def test_queue_sim_without_gpu(queue_exe):
+    r = subprocess.run([queue_exe], capture_output=True, text=True, env=_NOGPU, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "no gfx950 device" in r.stdout
+
+
+def test_extstore_sim_without_gpu(extstore_exe):
+    r = subprocess.run([extstore_exe], capture_output=True, text=True, env=_NOGPU, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "no gfx950 device" in r.stdout
+
+
+def _fields(line):
+    toks = line.split()
+    return {toks[i]: toks[i + 1] for i in range(len(toks) - 1)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads,reads,depth", [(16, 2000, 1), (8, 1000, 8), (1, 300, 1)])
+def test_queue_sim_many_io_threads(queue_exe, threads, reads, depth):
+    """io_depth-sized read batches from many threads: every CRC exact, every
+    torn read (and only those) detected, and the batches shared launches."""
+    r = subprocess.run([queue_exe, "--gpu", str(threads), str(reads), str(depth)], capture_output=True, text=True,
+                       timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    f = _fields(r.stdout)
+    assert int(f["mismatches"]) == 0 and int(f["false_bad"]) == 0 and f["detected"] == f["torn"]
+    assert int(f["spans"]) == threads * reads * depth
+    if threads > 1:
+        assert int(f["launches"]) < int(f["jobs"])  # coalesced
+
+
+@pytest.mark.gpu
+def test_extstore_sim_open_wbuf_fence(extstore_exe):
+    """Deferred stamping with the fence: reads of the open wbuf (and all
+    others) verify clean; every image ends with the scalar spill CRC."""
+    r = subprocess.run([extstore_exe, "--gpu", "8"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    f = _fields(r.stdout.replace(",", ""))
+    assert int(f["badcrc"]) == 0 and int(f["wbuf"].rstrip(")")) > 0
+
+
+@pytest.mark.gpu
+def test_extstore_sim_without_fence_sees_false_badcrc(extstore_exe):
+    """Negative control: the same run with the fence removed reports bad CRCs
+    for reads served from the open wbuf (the hole of a deferred stamp)."""
+    r = subprocess.run([extstore_exe, "--gpu", "--no-fence", "8"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert int(_fields(r.stdout.replace(",", ""))["badcrc"]) > 0
