@@ -51,6 +51,9 @@ extern "C" {
 #define CRC32C_ENOMEM (-4) /* device or pinned allocation failed */
 #define CRC32C_ERANGE (-5) /* a span lies outside [base, base + base_bytes): it was
                               not read and its out[] entry is 0 */
+#define CRC32C_EWALK (-6)  /* crc32c_verify_pages: the device walk's count and emit
+                              passes disagreed on some wbuf (an internal invariant;
+                              the results are not valid) */
 
 /* flags */
 #define CRC32C_DEVICE 0x1u    /* every pointer in the batch is device memory of the

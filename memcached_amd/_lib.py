@@ -20,6 +20,7 @@ CRC32C_EHIP = -2
 CRC32C_EINVAL = -3
 CRC32C_ENOMEM = -4
 CRC32C_ERANGE = -5
+CRC32C_EWALK = -6
 
 CRC32C_DEVICE = 0x1
 CRC32C_ASYNC = 0x2

@@ -1347,11 +1347,12 @@ constexpr uint32_t kWalkWaves = 4;  // waves (wbufs) per workgroup
 
 struct WalkOut {
     uint32_t *cnt;           // count pass: items per wbuf
-    const uint32_t *prefix;  // emit pass: index of each wbuf's first item
+    const uint32_t *prefix;  // emit pass: index of each wbuf's first item (nw + 1 entries)
     uint64_t *offs;          // emit pass: item offsets from base
     uint32_t *nunit;         // emit pass, planned verify (else nullptr): k_count's entries
     uint4 *irec;
     uint8_t *fast;
+    unsigned long long *err; // emit pass: wbufs whose two walks disagree (must stay 0)
 };
 
 // a: base, base_bytes (the walked bytes), region (= wbuf), and for the plan
@@ -1372,6 +1373,11 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
         const uint64_t start = w * wbuf, size = a.base_bytes - start < wbuf ? a.base_bytes - start : wbuf;
         const uint8_t *wb = a.base + start;
         const uint64_t first = EMIT ? out.prefix[w] : 0;
+        // the count pass's item count of this wbuf: the emit pass never writes
+        // past it (into the next wbuf's slots) and checks that it walks the
+        // same number of items (the walk invariant; see DESIGN.md section 3 on
+        // the round-2 readlane variants that broke it)
+        const uint64_t expect = EMIT ? out.prefix[w + 1] - first : 0;
         uint64_t off = 0, s = 0;  // wave-uniform: next item, stride guess (0: none yet)
         uint32_t c = 0;           // items walked so far
         while (off + 48 <= size) {
@@ -1394,7 +1400,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
             const uint64_t nt_m = (uint64_t)(uint32_t)__shfl((int)(uint32_t)nt, src, 64) |
                                   ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(nt >> 32), src, 64) << 32);
             const uint32_t k = m < 64u ? m + (last_item ? 1u : 0u) : 64u;  // items this round trip
-            if (EMIT && j < k) {
+            if (EMIT && j < k && c + j < expect) {
                 const uint64_t i = first + c + j;
                 out.offs[i] = start + o;
                 if (plan) count_item<1>(a, i, item_desc(a, start + o, h, true), t8, out.nunit, out.irec, out.fast);
@@ -1410,6 +1416,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
             }
         }
         if (!EMIT && j == 0) out.cnt[w] = c;
+        if (EMIT && j == 0 && c != expect) atomicAdd(out.err, 1ull);
     }
 }
 

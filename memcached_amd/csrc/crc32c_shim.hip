@@ -12,8 +12,13 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <memory>
@@ -70,8 +75,8 @@ struct Device {
     uint4 *img_k1 = nullptr;    // K1 image (160 KiB, crc32c_gf2.h build_lds_image_k1)
     uint32_t *xpow = nullptr;   // x^(8n) table (layout mcrc_dev::kXpow*)
     uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
-    unsigned long long *nbad = nullptr;
-    unsigned long long *hbad = nullptr;  // pinned twin of nbad (a D2H copy into pageable memory is a slow path)
+    unsigned long long *nbad = nullptr;  // [0]: bad / out-of-range count, [1]: walk invariant failures
+    unsigned long long *hbad = nullptr;  // pinned twin of nbad[0..1] (a D2H copy into pageable memory is a slow path)
     // k_small's own counters for calls that take the count from hbad (item
     // images): zero between calls, kept so by the kernel's last workgroup
     unsigned long long *small_nbad = nullptr;
@@ -236,8 +241,8 @@ int init_device(Device &d, int id) {
     HIP_OK(hipMemcpy(d.xpow, xp.data(), xp.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&d.zero, mcrc_dev::kZeroBytes));
     HIP_OK(hipMemset(d.zero, 0, mcrc_dev::kZeroBytes));
-    HIP_OK(hipMalloc(&d.nbad, sizeof(unsigned long long)));
-    HIP_OK(hipHostMalloc(&d.hbad, sizeof(unsigned long long), hipHostMallocDefault));
+    HIP_OK(hipMalloc(&d.nbad, 2 * sizeof(unsigned long long)));
+    HIP_OK(hipHostMalloc(&d.hbad, 2 * sizeof(unsigned long long), hipHostMallocDefault));
     HIP_OK(hipMalloc(&d.small_nbad, 16));
     HIP_OK(hipMemset(d.small_nbad, 0, 16));
     d.small_done = reinterpret_cast<uint32_t *>(d.small_nbad + 1);
@@ -912,11 +917,13 @@ struct crc32c_job {
 namespace {
 
 constexpr uint64_t kQueueSpanMax = 256u << 10;  // longer spans: the job runs alone (planned path)
+static_assert(sizeof(std::atomic<int>) == sizeof(int) && std::atomic<int>::is_always_lock_free,
+              "crc32c_job::done is waited on as a futex word");
 
 struct Queue {
     Device *d = nullptr;
     std::mutex mu;
-    std::condition_variable cv_work, cv_done;
+    std::condition_variable cv_work;
     std::deque<crc32c_job *> pending;
     hipStream_t st = nullptr;
     // pinned, mapped descriptors of one launch (kSmallMax spans each)
@@ -955,22 +962,23 @@ struct Queue {
         cv_work.notify_one();
     }
 
-    void complete(crc32c_job *j, int rc) {
+    // Completion wakes exactly the job's own waiter (a futex on j->done): with
+    // many IO threads a shared condition variable woke every waiter per launch,
+    // and spinning waiters starved the dispatcher of CPU time.
+    static void complete(crc32c_job *j, int rc) {
         j->rc = rc;
-        {
-            std::lock_guard<std::mutex> lk(mu);  // (no lost wake-up between a waiter's check and wait)
-            j->done.store(1, std::memory_order_release);
-        }
-        cv_done.notify_all();
+        j->done.store(1, std::memory_order_release);
+        syscall(SYS_futex, reinterpret_cast<int *>(&j->done), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
     }
 
-    int wait(crc32c_job *j) {
-        // completions come within tens of microseconds: spin a little first
-        for (int i = 0; i < 4096 && !j->done.load(std::memory_order_acquire); ++i) std::this_thread::yield();
-        if (!j->done.load(std::memory_order_acquire)) {
-            std::unique_lock<std::mutex> lk(mu);
-            cv_done.wait(lk, [&] { return j->done.load(std::memory_order_acquire) != 0; });
-        }
+    static int wait(crc32c_job *j) {
+        // a launch completes within tens of microseconds: spin briefly first
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!j->done.load(std::memory_order_acquire) &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(10))
+            __builtin_ia32_pause();
+        while (!j->done.load(std::memory_order_acquire))
+            syscall(SYS_futex, reinterpret_cast<int *>(&j->done), FUTEX_WAIT_PRIVATE, 0, nullptr, nullptr, 0);
         return j->rc;
     }
 
@@ -1138,6 +1146,7 @@ const char *crc32c_strerror(int err) {
         case CRC32C_EINVAL: return "invalid argument";
         case CRC32C_ENOMEM: return "out of device or pinned memory";
         case CRC32C_ERANGE: return "span outside [base, base + base_bytes) (not read)";
+        case CRC32C_EWALK: return "device page walk passes disagreed (results not valid)";
         default: return "unknown error";
     }
 }
@@ -1348,14 +1357,15 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     }
     wo.prefix = prefix;
     wo.offs = doffs;
+    wo.err = d->nbad + 1;
     wo.nunit = path.counted ? d->nunit : nullptr;
     wo.irec = path.counted ? d->irec : nullptr;
     wo.fast = path.counted ? d->fast : nullptr;
+    HIP_OK(hipMemsetAsync(d->nbad, 0, 2 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(mcrc_dev::k_walk<true>, dim3(gw), bw, 0, st, a, nw, wo);
-    HIP_OK(hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st));
     rc = launch_units<1>(*d, a, st, path);
     if (rc) return rc;
-    HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     const uint64_t k = std::min<uint64_t>(cap, total);
     if (!direct && k) {
         const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -1363,8 +1373,8 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
         HIP_OK(hipMemcpyAsync(ok, dok, k, kind, st));
     }
     HIP_OK(hipStreamSynchronize(st));
-    *nbad = *d->hbad;
-    return CRC32C_OK;
+    *nbad = d->hbad[0];
+    return d->hbad[1] ? CRC32C_EWALK : CRC32C_OK;
 }
 
 int crc32c_shard_cuts(const uint32_t *lens, uint32_t len, uint64_t n, int parts, uint64_t *cuts) {

@@ -133,40 +133,51 @@ void oracle_crc32c_batch(const unsigned char *base, const uint64_t *offsets, con
 #define ORACLE_ITEM_CAS 2u
 #define ORACLE_ITEM_CFLAGS 256u
 
-uint32_t oracle_item_ntotal(const unsigned char *it) {
+/* ITEM_ntotal with cfl = sizeof(client_flags_t): 4, or 8 in a build with
+ * --enable-large-client-flags (memcached.h:96-100, configure.ac:139-140). */
+uint32_t oracle_item_ntotal_cfl(const unsigned char *it, uint32_t cfl) {
     int32_t nbytes;
     uint16_t flags;
     memcpy(&nbytes, it + ORACLE_NBYTES_OFF, 4);
     memcpy(&flags, it + ORACLE_FLAGS_OFF, 2);
     uint32_t n = ORACLE_ITEM_HDR + it[ORACLE_NKEY_OFF] + 1u + (uint32_t)nbytes;
-    if (flags & ORACLE_ITEM_CFLAGS) n += 4;
+    if (flags & ORACLE_ITEM_CFLAGS) n += cfl;
     if (flags & ORACLE_ITEM_CAS) n += 8;
     return n;
 }
 
+uint32_t oracle_item_ntotal(const unsigned char *it) { return oracle_item_ntotal_cfl(it, 4); }
+
 /* Spill CRC of one item image (storage.c:567). */
-uint32_t oracle_item_crc(const unsigned char *it) {
-    return oracle_crc32c(0, it + ORACLE_STORE_OFFSET, oracle_item_ntotal(it) - ORACLE_STORE_OFFSET);
+uint32_t oracle_item_crc_cfl(const unsigned char *it, uint32_t cfl) {
+    return oracle_crc32c(0, it + ORACLE_STORE_OFFSET, oracle_item_ntotal_cfl(it, cfl) - ORACLE_STORE_OFFSET);
 }
+
+uint32_t oracle_item_crc(const unsigned char *it) { return oracle_item_crc_cfl(it, 4); }
 
 /* Walk one packed span the way storage.c:950-960 does and verify every item's
  * stored CRC (storage.c:160-178).  Returns the number of items; ok[i] = 1 when
  * the CRC matches; offsets[i] receives each item's offset.  max_items bounds
  * the output arrays. */
-uint64_t oracle_verify_span(const unsigned char *buf, uint64_t size, uint64_t *offsets,
-                            uint8_t *ok, uint64_t max_items) {
+uint64_t oracle_verify_span_cfl(const unsigned char *buf, uint64_t size, uint64_t *offsets,
+                                uint8_t *ok, uint64_t max_items, uint32_t cfl) {
     uint64_t off = 0, n = 0;
     while (off + ORACLE_ITEM_HDR <= size && n < max_items) {
         const unsigned char *it = buf + off;
         if (it[ORACLE_NKEY_OFF] == 0) break;
-        const uint32_t ntotal = oracle_item_ntotal(it);
+        const uint32_t ntotal = oracle_item_ntotal_cfl(it, cfl);
         if (off + ntotal > size) break;
         uint32_t stored;
         memcpy(&stored, it + ORACLE_EXPTIME_OFF, 4);
         offsets[n] = off;
-        ok[n] = stored == oracle_item_crc(it);
+        ok[n] = stored == oracle_item_crc_cfl(it, cfl);
         n++;
         off += ntotal;
     }
     return n;
+}
+
+uint64_t oracle_verify_span(const unsigned char *buf, uint64_t size, uint64_t *offsets,
+                            uint8_t *ok, uint64_t max_items) {
+    return oracle_verify_span_cfl(buf, size, offsets, ok, max_items, 4);
 }

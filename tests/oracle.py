@@ -33,9 +33,16 @@ def lib():
         L.oracle_crc32c_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_uint64]
         L.oracle_item_crc.restype = ctypes.c_uint32
         L.oracle_item_crc.argtypes = [ctypes.c_void_p]
+        L.oracle_item_crc_cfl.restype = ctypes.c_uint32
+        L.oracle_item_crc_cfl.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.oracle_item_ntotal_cfl.restype = ctypes.c_uint32
+        L.oracle_item_ntotal_cfl.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.oracle_verify_span.restype = ctypes.c_uint64
         L.oracle_verify_span.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_uint64]
+        L.oracle_verify_span_cfl.restype = ctypes.c_uint64
+        L.oracle_verify_span_cfl.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_uint64, ctypes.c_uint32]
         _lib = L
     return _lib
 
@@ -67,9 +74,16 @@ def batch(buf, offsets, lens, crc_in=None):
     return out
 
 
-def verify_span(buf, max_items=1 << 20):
+def verify_span(buf, max_items=1 << 20, cflags_bytes=4):
     buf = _arr(buf)
     offs = np.empty(max_items, np.uint64)
     ok = np.empty(max_items, np.uint8)
-    n = lib().oracle_verify_span(buf.ctypes.data, buf.size, offs.ctypes.data, ok.ctypes.data, max_items)
+    n = lib().oracle_verify_span_cfl(buf.ctypes.data, buf.size, offs.ctypes.data, ok.ctypes.data, max_items,
+                                     cflags_bytes)
     return offs[:n], ok[:n]
+
+
+def item_crc(buf, off, cflags_bytes=4):
+    """Spill CRC (storage.c:567) of the image at buf[off:]."""
+    buf = _arr(buf)
+    return int(lib().oracle_item_crc_cfl(buf.ctypes.data + int(off), cflags_bytes))

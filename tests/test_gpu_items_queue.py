@@ -1,0 +1,302 @@
+"""GPU parity, round 3: item images of LARGE_CLIENT_FLAGS builds, exact bad
+counts across consecutive small calls, host item calls on page-locked and
+pageable buffers (zero-copy and staged), the coalescing submit queue, the
+multi-GPU split and two ranks sharing the batch path.  Bit-exact against the
+CPU oracle."""
+import ctypes
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+try:  # GPU processes load torch (and its HIP runtime) before libmcrc32c.so
+    import torch as _torch  # noqa: F401
+except ImportError:
+    pass
+
+from memcached_amd import _lib, layout, shard
+from memcached_amd import crc32c as mc
+
+from . import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need a visible MI355X"
+    assert mc.gpu_count() >= 1, "libmcrc32c.so sees no gfx950 device"
+    return t
+
+
+@pytest.fixture(params=["small", "planned"])
+def span_path(request):
+    prev = mc.set_small_max(0 if request.param == "planned" else 8192)
+    yield request.param
+    mc.set_small_max(prev)
+
+
+def _pages(rng, n, wbuf, cfl, max_value=3000, flag_every=2):
+    items = [layout.make_item(b"key%07d" % i, rng.integers(0, 256, int(rng.integers(0, max_value)),
+                                                            dtype=np.uint8).tobytes(),
+                              cas=i + 1 if i % 5 else None,
+                              client_flags=(0x1_0000_0003 if cfl == 8 else 0x3) * (i % flag_every),
+                              cflags_bytes=cfl) for i in range(n)]
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    return buf, offs
+
+
+def _crcs(buf, offs, cfl):
+    return np.array([oracle.item_crc(buf, o, cfl) for o in offs], np.uint32)
+
+
+def _stored(buf, offs):
+    return buf[(offs[:, None].astype(np.int64) + np.arange(28, 32))].copy().view("<u4").reshape(-1)
+
+
+@pytest.mark.parametrize("cfl", [4, 8])
+def test_client_flags_width_items(torch, span_path, cfl):
+    """Verify, stamp and the device page walk over images whose ITEM_CFLAGS
+    suffix is 4 or 8 bytes (memcached.h:96-100, :149-152): exact with the
+    matching width, and the wrong width breaks flagged items."""
+    rng = np.random.default_rng(100 + cfl)
+    wbuf = 128 * 1024
+    buf, offs = _pages(rng, 400, wbuf, cfl)
+    want = _crcs(buf, offs, cfl)
+    layout.store_crcs(buf, offs, want)
+    wide = cfl == 8
+    d = torch.from_numpy(buf).cuda()
+    doffs = torch.from_numpy(offs.view(np.int64)).cuda()
+    ok, nbad = mc.verify_items(d, doffs, region_bytes=wbuf, cflags64=wide)
+    assert nbad == 0 and bool(ok.all())
+    ok_h, nbad_h = mc.verify_items(buf, offs, region_bytes=wbuf, cflags64=wide)
+    assert nbad_h == 0 and ok_h.all()
+    if wide:  # the 4-byte rule mis-sizes the flagged items (half of them)
+        _, nbad_w = mc.verify_items(d, doffs, region_bytes=wbuf, cflags64=False)
+        assert nbad_w >= (offs.size // 2) * 9 // 10
+    # stamp: exptime zeroed, then written by the library = the oracle's spill CRC
+    z = buf.copy()
+    layout.store_crcs(z, offs, np.zeros(offs.size, np.uint32))
+    dz = torch.from_numpy(z).cuda()
+    ok, nbad = mc.stamp_items(dz, doffs, region_bytes=wbuf, cflags64=wide)
+    torch.cuda.synchronize()
+    assert nbad == 0 and bool(ok.all())
+    np.testing.assert_array_equal(_stored(dz.cpu().numpy(), offs), want)
+    zh = z.copy()
+    ok, nbad = mc.stamp_items(zh, offs, region_bytes=wbuf, cflags64=wide)
+    assert nbad == 0 and ok.all()
+    np.testing.assert_array_equal(zh, buf)
+    # the device walk finds every image at its offset
+    w_offs, w_ok, w_bad = mc.verify_pages(d, wbuf, cflags64=wide)
+    np.testing.assert_array_equal(w_offs.cpu().numpy().astype(np.uint64), offs)
+    assert w_bad == 0 and bool(w_ok.all())
+
+
+@pytest.mark.parametrize("where", ["device", "host"])
+def test_small_verify_bad_counts_exact_across_calls(torch, where):
+    """k_small hands its bad count to the host through its last workgroup:
+    calls with thousands of bad items spread over every workgroup, alternated
+    with clean calls, must each report exactly their own count (an
+    add still in flight when the last workgroup read the counter was lost in
+    its call and counted in the next)."""
+    rng = np.random.default_rng(7)
+    wbuf = 4 << 20
+    buf, offs = _pages(rng, 2000, wbuf, 4, max_value=1500, flag_every=3)
+    layout.store_crcs(buf, offs, _crcs(buf, offs, 4))
+    bad = buf.copy()
+    victims = np.sort(rng.choice(offs.size, 1500, replace=False))
+    for v in victims:
+        bad[int(offs[v]) + 40] ^= 0x01  # pad byte 40 lies in the span: a CRC mismatch
+    assert buf.size <= 8 << 20  # the single-launch path
+    mk = (lambda a: torch.from_numpy(a).cuda()) if where == "device" else (lambda a: a)
+    clean_b, bad_b = mk(buf), mk(bad)
+    o = torch.from_numpy(offs.view(np.int64)).cuda() if where == "device" else offs
+    for rep in range(12):
+        ok, nbad = mc.verify_items(bad_b, o, region_bytes=wbuf)
+        assert nbad == victims.size, rep
+        okn = ok.cpu().numpy() if where == "device" else ok
+        np.testing.assert_array_equal(np.nonzero(okn == 0)[0], victims)
+        ok, nbad = mc.verify_items(clean_b, o, region_bytes=wbuf)
+        assert nbad == 0, rep
+
+
+def test_host_item_calls_pinned_pageable_and_large(torch):
+    """Host stamp / verify: page-locked buffers are read (and stamped) in place
+    by the kernel, also through an interior pointer; pageable ones through a
+    pinned copy; buffers past 8 MiB through the staged planned path."""
+    rng = np.random.default_rng(11)
+    wbuf = 1 << 20
+    buf, offs = _pages(rng, 900, wbuf, 4, max_value=2500)
+    want = _crcs(buf, offs, 4)
+    z = buf.copy()
+    layout.store_crcs(z, offs, np.zeros(offs.size, np.uint32))
+    ref = z.copy()
+    layout.store_crcs(ref, offs, want)
+    # pageable
+    zh = z.copy()
+    ok, nbad = mc.stamp_items(zh, offs, region_bytes=wbuf)
+    assert nbad == 0 and ok.all()
+    np.testing.assert_array_equal(zh, ref)
+    # page-locked, from the start and from an interior pointer (one wbuf in)
+    pin = torch.from_numpy(z.copy()).pin_memory()
+    pa = pin.numpy()
+    ok, nbad = mc.stamp_items(pa, offs, region_bytes=wbuf)
+    assert nbad == 0 and ok.all()
+    np.testing.assert_array_equal(pa, ref)
+    pin2 = torch.from_numpy(z.copy()).pin_memory()
+    tail = pin2.numpy()[wbuf:]
+    sel = offs >= wbuf
+    ok, nbad = mc.stamp_items(tail, offs[sel] - wbuf, region_bytes=wbuf)
+    assert nbad == 0 and ok.all()
+    np.testing.assert_array_equal(pin2.numpy()[wbuf:], ref[wbuf:])
+    assert (pin2.numpy()[:wbuf] == z[:wbuf]).all()
+    ok, nbad = mc.verify_items(pa, offs, region_bytes=wbuf)
+    assert nbad == 0 and ok.all()
+    # large (> 8 MiB): staged into device scratch, planned kernels
+    big_items = [layout.make_item(b"key%07d" % i, rng.integers(0, 256, 9000, dtype=np.uint8).tobytes())
+                 for i in range(1100)]
+    bb, bo = layout.pack_wbufs(big_items, wbuf)
+    assert bb.size > 8 << 20
+    bwant = _crcs(bb, bo, 4)
+    ok, nbad = mc.stamp_items(bb, bo, region_bytes=wbuf)
+    assert nbad == 0 and ok.all()
+    np.testing.assert_array_equal(_stored(bb, bo), bwant)
+    bb[int(bo[500]) + 100] ^= 4
+    ok, nbad = mc.verify_items(bb, bo, region_bytes=wbuf)
+    assert nbad == 1 and np.nonzero(ok == 0)[0].tolist() == [500]
+
+
+def _submit(spans, flags=0):
+    job = ctypes.c_void_p()
+    _lib.check(_lib.lib.crc32c_batch_submit(ctypes.byref(spans), flags, ctypes.byref(job)), "submit")
+    return job
+
+
+def test_queue_mixed_jobs_from_threads(torch):
+    """Jobs from 12 threads through crc32c_batch_submit / _wait: page-locked
+    host jobs (coalesced into shared launches), pageable host jobs and device
+    jobs (run alone by the dispatcher), chained with crc_in; every CRC exact."""
+    rng = np.random.default_rng(21)
+    size = 3 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    pin = torch.from_numpy(host).pin_memory()
+    dev = torch.from_numpy(host).cuda()
+    torch.cuda.synchronize()
+    l0, s0, j0, q0 = mc.queue_stats()
+    errors = []
+
+    def worker(t):
+        try:
+            r = np.random.default_rng(1000 + t)
+            for it in range(40):
+                n = int(r.integers(1, 9))
+                lens = r.integers(0, 70000, n).astype(np.uint32)
+                offs = np.array([int(r.integers(0, size - int(x))) for x in lens], np.uint64)
+                cin = r.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+                out = np.empty(n, np.uint32)
+                kind = (t + it) % 3
+                if kind == 2:  # device job: every array in device memory
+                    do = torch.from_numpy(offs.view(np.int64)).cuda()
+                    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+                    dc = torch.from_numpy(cin.view(np.int32)).cuda()
+                    dout = torch.empty(n, dtype=torch.int32, device="cuda")
+                    torch.cuda.synchronize()
+                    sp = _lib.Spans(dev.data_ptr(), size, do.data_ptr(), 0, dl.data_ptr(), 0, dc.data_ptr(),
+                                    dout.data_ptr(), n)
+                    _lib.check(_lib.lib.crc32c_batch_wait(_submit(sp, _lib.CRC32C_DEVICE)), "wait")
+                    out = dout.cpu().numpy().view(np.uint32)
+                else:
+                    base = pin.data_ptr() if kind == 0 else host.ctypes.data
+                    sp = _lib.Spans(base, size, offs.ctypes.data, 0, lens.ctypes.data, 0, cin.ctypes.data,
+                                    out.ctypes.data, n)
+                    _lib.check(_lib.lib.crc32c_batch_wait(_submit(sp)), "wait")
+                want = oracle.batch(host, offs, lens, cin)
+                if not (out == want).all():
+                    errors.append((t, it, kind))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:5]
+    l1, s1, j1, q1 = mc.queue_stats()
+    assert q1 - q0 == 2 * 160  # pageable + device jobs ran alone
+    assert j1 - j0 == 160 and l1 - l0 <= 160  # page-locked jobs, packed into launches
+
+
+def test_queue_rejects_out_of_range_host_spans(torch):
+    buf = np.zeros(4096, np.uint8)
+    offs = np.array([4000], np.uint64)
+    lens = np.array([200], np.uint32)
+    out = np.empty(1, np.uint32)
+    sp = _lib.Spans(buf.ctypes.data, buf.size, offs.ctypes.data, 0, lens.ctypes.data, 0, None, out.ctypes.data, 1)
+    job = ctypes.c_void_p()
+    assert _lib.lib.crc32c_batch_submit(ctypes.byref(sp), 0, ctypes.byref(job)) == _lib.CRC32C_EINVAL
+
+
+def test_batch_multi_matches_oracle(torch):
+    """crc32c_batch_multi on every visible device (the byte-balanced split of
+    crc32c_shard_cuts) over a Zipf-sized host batch."""
+    rng = np.random.default_rng(33)
+    lens = np.minimum(rng.zipf(1.3, 3000) * 64, 1 << 20).astype(np.uint32)
+    offs = np.concatenate([[3], 3 + np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    buf = rng.integers(0, 256, int(offs[-1] + lens[-1] + 5), dtype=np.uint8)
+    for ng in (1, 0):
+        got = mc.batch_multi(buf, offsets=offs, lens=lens, ngpus=ng)
+        np.testing.assert_array_equal(got, oracle.batch(buf, offs, lens))
+    np.testing.assert_array_equal(mc.shard_cuts(lens, 8), shard.plan(lens, 8))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from memcached_amd import crc32c as mcl
+    from memcached_amd import shard as sh
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(77)  # the same batch on every rank
+    lens = np.minimum(rng.zipf(1.2, 5000) * 32, 1 << 20).astype(np.uint32)
+    offs = np.concatenate([[1], 1 + np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    buf = rng.integers(0, 256, int(offs[-1] + lens[-1] + 1), dtype=np.uint8)
+    c = sh.plan(lens, world)
+    lo, hi = int(c[rank]), int(c[rank + 1])
+    d = torch.from_numpy(buf).cuda()  # each rank: its own copy, its own shard's spans
+    out = mcl.batch(d, offsets=torch.from_numpy(offs[lo:hi].view(np.int64)).cuda(),
+                    lens=torch.from_numpy(lens[lo:hi].view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    mine = out.cpu().numpy().view(np.uint32).tolist()
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (rank, lo, mine))
+    dist.destroy_process_group()
+    if rank == 0:
+        full = [x for _, _, part in sorted(gathered) for x in part]
+        q.put(full == [int(x) for x in oracle.batch(buf, offs, lens)])
+
+
+def test_two_ranks_device_batch_path(torch):
+    """Two processes (gloo for the exchange of results only), each checksumming
+    its shard of shard.plan through the device batch path on the GPU."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True

@@ -30,3 +30,21 @@ def test_pack_walk_roundtrip():
     buf[int(offs[7]) + 100] ^= 0x10
     o, ok = oracle.verify_span(buf[:64 * 1024])
     assert (~ok.astype(bool)).sum() == 1
+
+
+def test_large_client_flags_layout():
+    """A build with --enable-large-client-flags (memcached.h:96-100) makes
+    ITEM_CFLAGS add 8 bytes to ITEM_ntotal: walking such a page with the
+    4-byte rule mis-sizes every flagged item, with the 8-byte rule it is exact."""
+    rng = np.random.default_rng(5)
+    items = [layout.make_item(b"key%07d" % i, rng.integers(0, 256, int(rng.integers(1, 900)), dtype=np.uint8).tobytes(),
+                              cas=i + 1, client_flags=(i % 3) * 0x1_0000_0001, cflags_bytes=8) for i in range(200)]
+    assert len(items[1]) == layout.item_ntotal(10, len(items[1]) - 48 - 11 - 8 - 8, True, True, 8)
+    buf, offs = layout.pack_wbufs(items, 64 * 1024)
+    soffs, slens = layout.spans_of(buf, offs, cflags_bytes=8)
+    layout.store_crcs(buf, offs, oracle.batch(buf, soffs, slens))
+    o8, ok8 = oracle.verify_span(buf[:64 * 1024], cflags_bytes=8)
+    assert ok8.all() and [int(x) for x in o8] == [int(x) for x in offs if x < 64 * 1024]
+    o4, ok4 = oracle.verify_span(buf[:64 * 1024], cflags_bytes=4)
+    assert not (o4.size == o8.size and ok4.all())
+    assert oracle.item_crc(buf, offs[1], 8) == int.from_bytes(bytes(buf[int(offs[1]) + 28:int(offs[1]) + 32]), "little")

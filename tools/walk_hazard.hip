@@ -1,0 +1,214 @@
+// walk_hazard.hip -- dev experiment (not part of the library): why did the
+// SGPR/readlane form of the device page walk (round 2, commit 30e3f9d) count
+// large page sets wrongly and differently on each run?
+//
+// Count-pass variants of k_walk over the bench's config-5 page layout (4 MiB
+// wbufs of 1007 packed 4165-B images, zero tail, a few corrupt headers), each
+// run REPS times; every run's per-wbuf counts are compared with a host walk of
+// the same headers.
+//   V0  the shipped form: walk state in VGPRs, lane m broadcast by ds_bpermute
+//   V1  the round-2 failing form: lane m's flag and size read with v_readlane
+//       into SGPRs (wave-uniform scalar walk state)
+//   V2  V1 with 5 wait states (s_nop 4) between the ballot's VCC write and its
+//       SALU reads (s_ff1)
+//   V3  V1 with 5 wait states after each v_readlane before the SGPR is read
+//   V4  V1 with 5 wait states before each v_readlane (after the SALU write of
+//       its lane-select SGPR)
+//   V5  V1 with each v_readlane and 5 wait states after it in one asm
+//       statement (no SALU or VALU read of its SGPR within 5 states)
+//   V6  V5 with 5 more wait states before each v_readlane
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I memcached_amd/csrc tools/walk_hazard.hip -o /tmp/walk_hazard
+//   /tmp/walk_hazard PAGES REPS
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "crc32c_kernels.hip"
+
+using namespace mcrc_dev;
+
+#define CHECK(x)                                                                          \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));    \
+            exit(2);                                                                      \
+        }                                                                                 \
+    } while (0)
+
+template <int V>
+__global__ __launch_bounds__(64 * kWalkWaves) void k_count_v(SpanArgs a, uint64_t nw, uint32_t *cnt) {
+    const uint32_t j = threadIdx.x & 63u;
+    const uint64_t wbuf = a.region;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t w = (uint64_t)blockIdx.x * kWalkWaves + wave; w < nw; w += (uint64_t)gridDim.x * kWalkWaves) {
+        const uint64_t start = w * wbuf, size = a.base_bytes - start < wbuf ? a.base_bytes - start : wbuf;
+        const uint8_t *wb = a.base + start;
+        uint64_t off = 0, s = 0;
+        uint32_t c = 0;
+        while (off + 48 <= size) {
+            const uint64_t o = off + j * s;
+            const bool in = (j == 0 || s != 0) && o + 48 <= size;
+            ItemHdr h{0u, 0u, 0u, 0u};
+            if (in) h = parse_hdr(wb + o);
+            const uint64_t nt = h.ntotal(4);
+            const bool item = in && h.nkey != 0;
+            uint64_t brk = __ballot(!(item && nt == s));
+            if (V == 2) asm volatile("s_nop 4" : "+s"(brk));
+            const uint32_t m = brk ? (uint32_t)__ffsll((unsigned long long)brk) - 1u : 64u;
+            bool last_item = false;
+            uint64_t nt_m = 0;
+            if (V == 0) {
+                const int src = m < 64u ? (int)m : 0;
+                last_item = m < 64u && __shfl((int)item, src, 64) != 0;
+                nt_m = (uint64_t)(uint32_t)__shfl((int)(uint32_t)nt, src, 64) |
+                       ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(nt >> 32), src, 64) << 32);
+            } else if (V >= 5 && m < 64u) {
+                int li, lo, hi;
+                const int iv = (int)item, lov = (int)(uint32_t)nt, hiv = (int)(uint32_t)(nt >> 32);
+                if (V == 5) {
+                    asm volatile("v_readlane_b32 %0, %1, %2\n\ts_nop 4" : "=s"(li) : "v"(iv), "s"(m));
+                    asm volatile("v_readlane_b32 %0, %1, %2\n\ts_nop 4" : "=s"(lo) : "v"(lov), "s"(m));
+                    asm volatile("v_readlane_b32 %0, %1, %2\n\ts_nop 4" : "=s"(hi) : "v"(hiv), "s"(m));
+                } else {
+                    asm volatile("s_nop 4\n\tv_readlane_b32 %0, %1, %2\n\ts_nop 4" : "=s"(li) : "v"(iv), "s"(m));
+                    asm volatile("s_nop 4\n\tv_readlane_b32 %0, %1, %2\n\ts_nop 4" : "=s"(lo) : "v"(lov), "s"(m));
+                    asm volatile("s_nop 4\n\tv_readlane_b32 %0, %1, %2\n\ts_nop 4" : "=s"(hi) : "v"(hiv), "s"(m));
+                }
+                last_item = li != 0;
+                nt_m = (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+            } else if (m < 64u) {
+                int mm = (int)m;
+                if (V == 4) asm volatile("s_nop 4" : "+s"(mm));
+                int li = __builtin_amdgcn_readlane((int)item, mm);
+                int lo = __builtin_amdgcn_readlane((int)(uint32_t)nt, mm);
+                int hi = __builtin_amdgcn_readlane((int)(uint32_t)(nt >> 32), mm);
+                if (V == 3) asm volatile("s_nop 4" : "+s"(li), "+s"(lo), "+s"(hi));
+                last_item = li != 0;
+                nt_m = (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+            }
+            const uint32_t k = m < 64u ? m + (last_item ? 1u : 0u) : 64u;
+            c += k;
+            if (m == 64u) {
+                off += 64u * s;
+            } else if (!last_item) {
+                break;
+            } else {
+                off += m * s + nt_m;
+                s = nt_m;
+            }
+        }
+        if (j == 0) cnt[w] = c;
+    }
+}
+
+// config-5 layout: item i of wbuf w at w * wbuf + i * 4165; header fields as
+// bench.py workload_config5; `bad` items get a flipped bit in nbytes / nkey.
+__global__ void k_fill(uint8_t *base, uint64_t nwb, uint64_t wbuf, uint32_t seed) {
+    const uint64_t n = nwb * 1007;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint8_t *it = base + (i / 1007) * wbuf + (i % 1007) * 4165;
+        uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+        x ^= x >> 15;
+        x *= 0x2c1b3c6du;
+        x ^= x >> 12;
+        uint32_t nbytes = 4098;
+        uint8_t nkey = 10;
+        if (x % 3000 == 7) nbytes ^= 1u << (x >> 20) % 20;  // a corrupt length
+        if (x % 7000 == 11) nkey = 0;                       // a zeroed key length
+        memcpy(it + 32, &nbytes, 4);
+        it[36] = 1;
+        it[37] = 0;
+        it[38] = 2;  // ITEM_CAS
+        it[39] = 0;
+        it[40] = 17;
+        it[41] = nkey;
+    }
+}
+
+static uint32_t host_walk(const uint8_t *h, uint64_t size) {
+    uint64_t off = 0;
+    uint32_t c = 0;
+    while (off + 48 <= size) {
+        const uint8_t *it = h + off;
+        if (it[41] == 0) break;
+        uint32_t nbytes;
+        uint16_t flags;
+        memcpy(&nbytes, it + 32, 4);
+        memcpy(&flags, it + 38, 2);
+        const uint64_t nt = 48ull + it[41] + 1 + nbytes + ((flags & 256) ? 4 : 0) + ((flags & 2) ? 8 : 0);
+        ++c;
+        off += nt;
+    }
+    return c;
+}
+
+int main(int argc, char **argv) {
+    const uint64_t pages = argc > 1 ? strtoull(argv[1], nullptr, 10) : 300;
+    const int reps = argc > 2 ? atoi(argv[2]) : 3;
+    const uint64_t wbuf = 4ull << 20, nwb = pages * 16, bytes = nwb * wbuf;
+    uint8_t *d = nullptr;
+    CHECK(hipMalloc(&d, bytes));
+    CHECK(hipMemset(d, 0x5a, bytes));
+    for (uint64_t w = 0; w < nwb; ++w) CHECK(hipMemset(d + w * wbuf + 1007 * 4165, 0, wbuf - 1007 * 4165));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, d, nwb, wbuf, 12345u);
+    CHECK(hipDeviceSynchronize());
+    // host walk of every wbuf (headers only matter; copy wbuf by wbuf)
+    std::vector<uint32_t> want(nwb);
+    std::vector<uint8_t> hb(wbuf);
+    uint64_t total = 0;
+    for (uint64_t w = 0; w < nwb; ++w) {
+        CHECK(hipMemcpy(hb.data(), d + w * wbuf, wbuf, hipMemcpyDeviceToHost));
+        want[w] = host_walk(hb.data(), wbuf);
+        total += want[w];
+    }
+    printf("pages %llu wbufs %llu items (host walk) %llu\n", (unsigned long long)pages, (unsigned long long)nwb,
+           (unsigned long long)total);
+    uint32_t *cnt = nullptr;
+    CHECK(hipMalloc(&cnt, nwb * 4));
+    std::vector<uint32_t> got(nwb);
+    SpanArgs a{};
+    a.base = d;
+    a.base_bytes = bytes;
+    a.region = wbuf;
+    a.cfl = 4;
+    const int gw = (int)std::min<uint64_t>((nwb + kWalkWaves - 1) / kWalkWaves, 65535);
+    auto run = [&](int v) {
+        CHECK(hipMemset(cnt, 0xff, nwb * 4));
+        switch (v) {
+            case 0: hipLaunchKernelGGL(k_count_v<0>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 1: hipLaunchKernelGGL(k_count_v<1>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 2: hipLaunchKernelGGL(k_count_v<2>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 3: hipLaunchKernelGGL(k_count_v<3>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 4: hipLaunchKernelGGL(k_count_v<4>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 5: hipLaunchKernelGGL(k_count_v<5>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            default: hipLaunchKernelGGL(k_count_v<6>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+        }
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipMemcpy(got.data(), cnt, nwb * 4, hipMemcpyDeviceToHost));
+        uint64_t bad = 0, sum = 0;
+        int64_t first = -1;
+        for (uint64_t w = 0; w < nwb; ++w) {
+            sum += got[w];
+            if (got[w] != want[w]) {
+                ++bad;
+                if (first < 0) first = (int64_t)w;
+            }
+        }
+        printf("V%d: items %llu, wbufs wrong %llu", v, (unsigned long long)sum, (unsigned long long)bad);
+        if (first >= 0) {
+            printf(" (first: wbuf %lld got %u want %u; next %u/%u)", (long long)first, got[first], want[first],
+                   first + 1 < (int64_t)nwb ? got[first + 1] : 0u, first + 1 < (int64_t)nwb ? want[first + 1] : 0u);
+        }
+        printf("\n");
+        fflush(stdout);
+    };
+    for (int r = 0; r < reps; ++r)
+        for (int v = 0; v <= 6; ++v) run(v);
+    CHECK(hipFree(cnt));
+    CHECK(hipFree(d));
+    return 0;
+}
