@@ -926,10 +926,16 @@ struct Queue {
     std::condition_variable cv_work;
     std::deque<crc32c_job *> pending;
     hipStream_t st = nullptr;
-    // pinned, mapped descriptors of one launch (kSmallMax spans each)
-    uint64_t *addr = nullptr;
-    uint32_t *len = nullptr, *cin = nullptr, *out = nullptr;
-    void *v_addr = nullptr, *v_len = nullptr, *v_cin = nullptr, *v_out = nullptr;
+    // Two launch slots: while one launch runs, the next (whatever was pending
+    // when it started) is queued behind it on the stream.  Each slot has
+    // pinned, mapped descriptors for kSmallMax spans and its event.
+    struct Slot {
+        uint64_t *addr = nullptr;
+        uint32_t *len = nullptr, *cin = nullptr, *out = nullptr;
+        void *v_addr = nullptr, *v_len = nullptr, *v_cin = nullptr, *v_out = nullptr;
+        hipEvent_t done = nullptr;
+        std::vector<crc32c_job *> jobs;  // empty: the slot is free
+    } slot[2];
     unsigned long long *dnbad = nullptr;  // (spans are absolute: never out of range)
     std::atomic<uint64_t> launches{0}, spans{0}, jobs{0}, solo{0};
 
@@ -938,14 +944,17 @@ struct Queue {
         HIP_OK(hipSetDevice(dev.id));
         HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
         const uint64_t n = mcrc_dev::kSmallMax;
-        HIP_OK(hipHostMalloc((void **)&addr, n * 8, hipHostMallocDefault));
-        HIP_OK(hipHostMalloc((void **)&len, n * 4, hipHostMallocDefault));
-        HIP_OK(hipHostMalloc((void **)&cin, n * 4, hipHostMallocDefault));
-        HIP_OK(hipHostMalloc((void **)&out, n * 4, hipHostMallocDefault));
-        HIP_OK(hipHostGetDevicePointer(&v_addr, addr, 0));
-        HIP_OK(hipHostGetDevicePointer(&v_len, len, 0));
-        HIP_OK(hipHostGetDevicePointer(&v_cin, cin, 0));
-        HIP_OK(hipHostGetDevicePointer(&v_out, out, 0));
+        for (Slot &l : slot) {
+            HIP_OK(hipHostMalloc((void **)&l.addr, n * 8, hipHostMallocDefault));
+            HIP_OK(hipHostMalloc((void **)&l.len, n * 4, hipHostMallocDefault));
+            HIP_OK(hipHostMalloc((void **)&l.cin, n * 4, hipHostMallocDefault));
+            HIP_OK(hipHostMalloc((void **)&l.out, n * 4, hipHostMallocDefault));
+            HIP_OK(hipHostGetDevicePointer(&l.v_addr, l.addr, 0));
+            HIP_OK(hipHostGetDevicePointer(&l.v_len, l.len, 0));
+            HIP_OK(hipHostGetDevicePointer(&l.v_cin, l.cin, 0));
+            HIP_OK(hipHostGetDevicePointer(&l.v_out, l.out, 0));
+            HIP_OK(hipEventCreateWithFlags(&l.done, hipEventDisableTiming));
+        }
         HIP_OK(hipMalloc(&dnbad, sizeof(unsigned long long)));
         HIP_OK(hipMemset(dnbad, 0, sizeof(unsigned long long)));
         // the dispatcher lives as long as the process (never joined: the queue
@@ -982,24 +991,25 @@ struct Queue {
         return j->rc;
     }
 
-    // Every job of `batch` in one k_small launch over absolute span addresses.
-    int launch(const std::vector<crc32c_job *> &batch) {
+    // The jobs of slot l in one k_small launch over absolute span addresses
+    // (enqueued, not waited for).
+    int launch(Slot &l) {
         uint64_t k = 0;
-        for (crc32c_job *j : batch) {
+        for (crc32c_job *j : l.jobs) {
             const crc32c_spans &s = j->s;
             for (uint64_t i = 0; i < s.n; ++i, ++k) {
-                addr[k] = (uint64_t)(uintptr_t)(j->dbase + span_off(s, i));
-                len[k] = (uint32_t)span_len(s, i);
-                cin[k] = s.crc_in ? s.crc_in[i] : 0u;
+                l.addr[k] = (uint64_t)(uintptr_t)(j->dbase + span_off(s, i));
+                l.len[k] = (uint32_t)span_len(s, i);
+                l.cin[k] = s.crc_in ? s.crc_in[i] : 0u;
             }
         }
         mcrc_dev::SpanArgs a{};
         a.base = nullptr;  // spans at absolute addresses
         a.base_bytes = ~0ull;
-        a.offsets = (const uint64_t *)v_addr;
-        a.lens = (const uint32_t *)v_len;
-        a.crc_in = (const uint32_t *)v_cin;
-        a.out = (uint32_t *)v_out;
+        a.offsets = (const uint64_t *)l.v_addr;
+        a.lens = (const uint32_t *)l.v_len;
+        a.crc_in = (const uint32_t *)l.v_cin;
+        a.out = (uint32_t *)l.v_out;
         a.nbad = dnbad;
         a.n = k;
         a.xpow = d->xpow;
@@ -1008,16 +1018,23 @@ struct Queue {
         a.cfl = 4;
         int rc = launch_small<0>(*d, a, st);
         if (rc) return rc;
-        HIP_OK(hipStreamSynchronize(st));
-        k = 0;
-        for (crc32c_job *j : batch) {
-            memcpy(j->s.out, out + k, j->s.n * 4);
-            k += j->s.n;
-        }
+        HIP_OK(hipEventRecord(l.done, st));
         launches.fetch_add(1, std::memory_order_relaxed);
         spans.fetch_add(k, std::memory_order_relaxed);
-        jobs.fetch_add(batch.size(), std::memory_order_relaxed);
+        jobs.fetch_add(l.jobs.size(), std::memory_order_relaxed);
         return CRC32C_OK;
+    }
+
+    // Wait for slot l's launch, hand out the CRCs, wake the waiters.
+    void finish(Slot &l, int rc) {
+        if (!rc && hipEventSynchronize(l.done) != hipSuccess) rc = CRC32C_EHIP;
+        uint64_t k = 0;
+        for (crc32c_job *j : l.jobs) {
+            if (!rc) memcpy(j->s.out, l.out + k, j->s.n * 4);
+            k += j->s.n;
+            complete(j, rc);
+        }
+        l.jobs.clear();
     }
 
     int run_solo(crc32c_job *j) {
@@ -1028,31 +1045,34 @@ struct Queue {
 
     void run() {
         (void)hipSetDevice(d->id);
-        std::vector<crc32c_job *> batch;
+        int cur = 0;              // slot of the launch in flight (if it has jobs)
+        int rcs[2] = {0, 0};      // launch status of each slot
         for (;;) {
+            Slot &busy = slot[cur], &next = slot[cur ^ 1];
+            crc32c_job *solo_job = nullptr;
             {
                 std::unique_lock<std::mutex> lk(mu);
-                cv_work.wait(lk, [&] { return !pending.empty(); });
-                batch.clear();
-                if (!pending.front()->coalesce) {
-                    batch.push_back(pending.front());
+                if (busy.jobs.empty()) cv_work.wait(lk, [&] { return !pending.empty(); });
+                if (!pending.empty() && !pending.front()->coalesce) {
+                    solo_job = pending.front();
                     pending.pop_front();
                 } else {
                     uint64_t ns = 0;
                     while (!pending.empty() && pending.front()->coalesce &&
                            ns + pending.front()->s.n <= mcrc_dev::kSmallMax) {
                         ns += pending.front()->s.n;
-                        batch.push_back(pending.front());
+                        next.jobs.push_back(pending.front());
                         pending.pop_front();
                     }
                 }
             }
-            if (!batch[0]->coalesce) {
-                complete(batch[0], run_solo(batch[0]));
-                continue;
+            if (!next.jobs.empty()) rcs[cur ^ 1] = launch(next);  // queued behind the busy slot
+            if (!busy.jobs.empty()) finish(busy, rcs[cur]);
+            if (solo_job) {  // (the stream is drained first: solo jobs use it too)
+                if (!next.jobs.empty()) finish(next, rcs[cur ^ 1]);
+                complete(solo_job, run_solo(solo_job));
             }
-            const int rc = launch(batch);
-            for (crc32c_job *j : batch) complete(j, rc);
+            cur ^= 1;
         }
     }
 };

@@ -17,6 +17,8 @@
 //   V5  V1 with each v_readlane and 5 wait states after it in one asm
 //       statement (no SALU or VALU read of its SGPR within 5 states)
 //   V6  V5 with 5 more wait states before each v_readlane
+//   V7  V1 recording, per wbuf, its first four round trips (off, s, m, k,
+//       lane 0's header fields) for the post-mortem of a wrong wbuf
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I memcached_amd/csrc tools/walk_hazard.hip -o /tmp/walk_hazard
 //   /tmp/walk_hazard PAGES REPS
@@ -39,6 +41,8 @@ using namespace mcrc_dev;
         }                                                                                 \
     } while (0)
 
+__device__ uint32_t *g_trace;  // V7: [wbuf][round 0..3][8 dwords]
+
 template <int V>
 __global__ __launch_bounds__(64 * kWalkWaves) void k_count_v(SpanArgs a, uint64_t nw, uint32_t *cnt) {
     const uint32_t j = threadIdx.x & 63u;
@@ -48,7 +52,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_count_v(SpanArgs a, uint64_
         const uint64_t start = w * wbuf, size = a.base_bytes - start < wbuf ? a.base_bytes - start : wbuf;
         const uint8_t *wb = a.base + start;
         uint64_t off = 0, s = 0;
-        uint32_t c = 0;
+        uint32_t c = 0, round = 0;
         while (off + 48 <= size) {
             const uint64_t o = off + j * s;
             const bool in = (j == 0 || s != 0) && o + 48 <= size;
@@ -91,6 +95,22 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_count_v(SpanArgs a, uint64_
                 nt_m = (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
             }
             const uint32_t k = m < 64u ? m + (last_item ? 1u : 0u) : 64u;
+            if (V == 7 && round < 4) {
+                uint32_t *t = g_trace + (w * 4 + round) * 8;
+                const uint32_t l0nb = __shfl(h.nbytes, 0, 64), l0nk = __shfl(h.nkey, 0, 64);
+                const uint32_t l0nt = (uint32_t)__shfl((int)(uint32_t)nt, 0, 64);
+                if (j == 0) {
+                    t[0] = (uint32_t)off;
+                    t[1] = (uint32_t)s;
+                    t[2] = m | (last_item ? 0x100u : 0u) | (k << 16);
+                    t[3] = (uint32_t)nt_m;
+                    t[4] = (uint32_t)brk;
+                    t[5] = (uint32_t)(brk >> 32);
+                    t[6] = l0nb | (l0nk << 24);
+                    t[7] = l0nt;
+                }
+            }
+            ++round;
             c += k;
             if (m == 64u) {
                 off += 64u * s;
@@ -167,8 +187,11 @@ int main(int argc, char **argv) {
     }
     printf("pages %llu wbufs %llu items (host walk) %llu\n", (unsigned long long)pages, (unsigned long long)nwb,
            (unsigned long long)total);
-    uint32_t *cnt = nullptr;
+    uint32_t *cnt = nullptr, *trace = nullptr;
     CHECK(hipMalloc(&cnt, nwb * 4));
+    CHECK(hipMalloc(&trace, nwb * 32 * 4));
+    CHECK(hipMemset(trace, 0xee, nwb * 32 * 4));
+    CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &trace, sizeof trace));
     std::vector<uint32_t> got(nwb);
     SpanArgs a{};
     a.base = d;
@@ -185,7 +208,8 @@ int main(int argc, char **argv) {
             case 3: hipLaunchKernelGGL(k_count_v<3>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
             case 4: hipLaunchKernelGGL(k_count_v<4>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
             case 5: hipLaunchKernelGGL(k_count_v<5>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
-            default: hipLaunchKernelGGL(k_count_v<6>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 6: hipLaunchKernelGGL(k_count_v<6>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            default: hipLaunchKernelGGL(k_count_v<7>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
         }
         CHECK(hipDeviceSynchronize());
         CHECK(hipMemcpy(got.data(), cnt, nwb * 4, hipMemcpyDeviceToHost));
@@ -204,10 +228,26 @@ int main(int argc, char **argv) {
                    first + 1 < (int64_t)nwb ? got[first + 1] : 0u, first + 1 < (int64_t)nwb ? want[first + 1] : 0u);
         }
         printf("\n");
+        if (v == 7 && bad) {  // the first three wrong wbufs' round trips
+            std::vector<uint32_t> tr(nwb * 32);
+            CHECK(hipMemcpy(tr.data(), trace, nwb * 32 * 4, hipMemcpyDeviceToHost));
+            int shown = 0;
+            for (uint64_t w = 0; w < nwb && shown < 3; ++w) {
+                if (got[w] == want[w]) continue;
+                ++shown;
+                printf("  wbuf %llu got %u want %u\n", (unsigned long long)w, got[w], want[w]);
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t *t = &tr[(w * 4 + r) * 8];
+                    printf("    round %d: off %u s %u m %u last %u k %u nt_m %u brk %08x%08x lane0 nbytes %u nkey %u nt %u\n",
+                           r, t[0], t[1], t[2] & 0xff, (t[2] >> 8) & 1, t[2] >> 16, t[3], t[5], t[4], t[6] & 0xffffff,
+                           t[6] >> 24, t[7]);
+                }
+            }
+        }
         fflush(stdout);
     };
     for (int r = 0; r < reps; ++r)
-        for (int v = 0; v <= 6; ++v) run(v);
+        for (int v = 0; v <= 7; ++v) run(v);
     CHECK(hipFree(cnt));
     CHECK(hipFree(d));
     return 0;
