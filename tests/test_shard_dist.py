@@ -1,8 +1,11 @@
 """Multi-rank path on CPU: world_size 2 over gloo.
 
-Each rank checksums only its own shard (the product's host scalar CRC), no data
-is exchanged on the compute path; the test then gathers the shards to check
-they tile the batch exactly and match the oracle.
+Each rank checksums only its own shard (the product's host scalar CRC here:
+there is no GPU on this host; tests/test_gpu_items_queue.py runs two ranks
+through the batch path on the GPU), no data is exchanged on the compute path;
+the test then gathers the shards to check they tile the batch exactly and
+match the oracle.  The C split (crc32c_shard_cuts, used by
+crc32c_batch_multi) is checked against shard.plan here too: it is host code.
 """
 import os
 import socket
@@ -30,6 +33,22 @@ def test_plan_balances_bytes_and_tiles():
         per = [int(lens[c[r]:c[r + 1]].sum()) for r in range(world)]
         assert max(per) - min(per) <= 2 * int(lens.max())
     assert list(shard.plan_equal(8 << 20, 8)) == [i << 20 for i in range(9)]
+
+
+def test_c_shard_cuts_equal_plan():
+    """crc32c_shard_cuts (C, 128-bit prefix) and shard.plan (numpy) give the
+    same cut points: Zipf lengths for 1-8 parts, equal lengths, zero-length
+    spans, fewer spans than parts, an empty batch."""
+    from memcached_amd import crc32c as mc
+    rng = np.random.default_rng(7)
+    zipf = np.minimum(rng.zipf(1.3, 20000) * 64, 1 << 20).astype(np.uint32)
+    cases = [zipf, np.full(1000, 4096, np.uint32), np.zeros(50, np.uint32),
+             np.array([5, 0, 0, 7, 1 << 20], np.uint32), np.array([9], np.uint32), np.zeros(0, np.uint32)]
+    for lens in cases:
+        for parts in range(1, 9):
+            got = mc.shard_cuts(lens, parts)
+            np.testing.assert_array_equal(got, shard.plan(lens.astype(np.uint64), parts))
+            assert got[0] == 0 and got[-1] == lens.size and (np.diff(got) >= 0).all()
 
 
 def _worker(rank, world, port, q):

@@ -19,8 +19,20 @@
 //   V6  V5 with 5 more wait states before each v_readlane
 //   V7  V1 recording, per wbuf, its first four round trips (off, s, m, k,
 //       lane 0's header fields) for the post-mortem of a wrong wbuf
+//   V8  V1 with the lane's header offset in 32-bit arithmetic (off + j * s
+//       < 4 GiB in a wbuf): no v_mad_u64_u32, whose carry-out SGPR pair the
+//       compiler reuses 5 instructions later for an s_cselect in V1-V7
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I memcached_amd/csrc tools/walk_hazard.hip -o /tmp/walk_hazard
+//   V1 at 1 and 2 workgroups per CU (dynamic LDS of 100 and 64 KiB, nothing
+//   else changed): whether the failures need waves of several workgroups
+//   sharing a SIMD
+//
+// and a register-level test of that pattern (k_waw): v_mad_u64_u32 with its
+// carry-out in an SGPR pair, three VALU instructions, then an SALU write
+// (s_cselect_b64 -1) of the same pair, which must read back -1; P = the
+// number of s_nop 7 between them (0: the sequence of V1-V7)
+//
+//   bash tools/walk_hazard.sh OUT  (or: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I memcached_amd/csrc tools/walk_hazard.hip -o /tmp/walk_hazard)
 //   /tmp/walk_hazard PAGES REPS
 #include <stdio.h>
 #include <stdlib.h>
@@ -70,7 +82,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_count_v(SpanArgs a, uint64_
                 last_item = m < 64u && __shfl((int)item, src, 64) != 0;
                 nt_m = (uint64_t)(uint32_t)__shfl((int)(uint32_t)nt, src, 64) |
                        ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(nt >> 32), src, 64) << 32);
-            } else if (V >= 5 && m < 64u) {
+            } else if (V >= 5 && V <= 7 && m < 64u) {
                 int li, lo, hi;
                 const int iv = (int)item, lov = (int)(uint32_t)nt, hiv = (int)(uint32_t)(nt >> 32);
                 if (V == 5) {
@@ -149,6 +161,45 @@ __global__ void k_fill(uint8_t *base, uint64_t nwb, uint64_t wbuf, uint32_t seed
     }
 }
 
+template <int P>
+__global__ __launch_bounds__(256) void k_waw(unsigned long long *bad, uint32_t iters, uint32_t s_lo, uint32_t s_hi,
+                                             uint64_t sv) {
+    const uint32_t j = threadIdx.x & 63u;
+    uint64_t acc = (uint64_t)blockIdx.x << 20;
+    uint32_t nb = 0;
+    for (uint32_t i = 0; i < iters; ++i) {
+        uint64_t flag;
+        uint32_t t0, t1;
+        if (P == 0)
+            asm volatile(
+                "v_mad_u64_u32 %0, %1, %4, %5, %0\n\t"
+                "v_mul_lo_u32 %2, %4, 0\n\t"
+                "v_mul_lo_u32 %3, %6, %5\n\t"
+                "v_add_u32 %3, %3, %2\n\t"
+                "s_cmp_lg_u64 %7, 0\n\t"
+                "s_cselect_b64 %1, -1, 0"
+                : "+v"(acc), "=&s"(flag), "=&v"(t0), "=&v"(t1)
+                : "s"(s_lo), "v"(j), "s"(s_hi), "s"(sv)
+                : "scc");
+        else
+            asm volatile(
+                "v_mad_u64_u32 %0, %1, %4, %5, %0\n\t"
+                "v_mul_lo_u32 %2, %4, 0\n\t"
+                "v_mul_lo_u32 %3, %6, %5\n\t"
+                "v_add_u32 %3, %3, %2\n\t"
+                "s_nop 7\n\ts_nop 7\n\t"
+                "s_cmp_lg_u64 %7, 0\n\t"
+                "s_cselect_b64 %1, -1, 0"
+                : "+v"(acc), "=&s"(flag), "=&v"(t0), "=&v"(t1)
+                : "s"(s_lo), "v"(j), "s"(s_hi), "s"(sv)
+                : "scc");
+        nb += flag != ~0ull;
+        acc += t1 & 1u;
+    }
+    if (j == 0 && nb) atomicAdd(bad, (unsigned long long)nb);
+    if (acc == 0x123456789ull) atomicAdd(bad, 1ull << 40);  // (keeps acc live)
+}
+
 static uint32_t host_walk(const uint8_t *h, uint64_t size) {
     uint64_t off = 0;
     uint32_t c = 0;
@@ -199,17 +250,21 @@ int main(int argc, char **argv) {
     a.region = wbuf;
     a.cfl = 4;
     const int gw = (int)std::min<uint64_t>((nwb + kWalkWaves - 1) / kWalkWaves, 65535);
-    auto run = [&](int v) {
+    CHECK(hipFuncSetAttribute((const void *)k_count_v<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 100 << 10));
+    auto run = [&](int v, int lds_kib = 0) {
         CHECK(hipMemset(cnt, 0xff, nwb * 4));
         switch (v) {
             case 0: hipLaunchKernelGGL(k_count_v<0>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
-            case 1: hipLaunchKernelGGL(k_count_v<1>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 1:
+                hipLaunchKernelGGL(k_count_v<1>, dim3(gw), dim3(64 * kWalkWaves), lds_kib << 10, 0, a, nwb, cnt);
+                break;
             case 2: hipLaunchKernelGGL(k_count_v<2>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
             case 3: hipLaunchKernelGGL(k_count_v<3>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
             case 4: hipLaunchKernelGGL(k_count_v<4>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
             case 5: hipLaunchKernelGGL(k_count_v<5>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
             case 6: hipLaunchKernelGGL(k_count_v<6>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
-            default: hipLaunchKernelGGL(k_count_v<7>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 7: hipLaunchKernelGGL(k_count_v<7>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            default: hipLaunchKernelGGL(k_count_v<8>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
         }
         CHECK(hipDeviceSynchronize());
         CHECK(hipMemcpy(got.data(), cnt, nwb * 4, hipMemcpyDeviceToHost));
@@ -222,7 +277,9 @@ int main(int argc, char **argv) {
                 if (first < 0) first = (int64_t)w;
             }
         }
-        printf("V%d: items %llu, wbufs wrong %llu", v, (unsigned long long)sum, (unsigned long long)bad);
+        printf("V%d%s: items %llu, wbufs wrong %llu", v,
+               lds_kib == 100 ? " (1 workgroup per CU)" : lds_kib == 64 ? " (2 workgroups per CU)" : "",
+               (unsigned long long)sum, (unsigned long long)bad);
         if (first >= 0) {
             printf(" (first: wbuf %lld got %u want %u; next %u/%u)", (long long)first, got[first], want[first],
                    first + 1 < (int64_t)nwb ? got[first + 1] : 0u, first + 1 < (int64_t)nwb ? want[first + 1] : 0u);
@@ -246,8 +303,31 @@ int main(int argc, char **argv) {
         }
         fflush(stdout);
     };
-    for (int r = 0; r < reps; ++r)
-        for (int v = 0; v <= 7; ++v) run(v);
+    // the register-level test: 2048 blocks of 4 waves (8 per CU), 20000
+    // sequences per wave, with and without the pad
+    unsigned long long *dbad = nullptr;
+    CHECK(hipMalloc(&dbad, 8));
+    for (int r = 0; r < reps; ++r) {
+        for (int pad = 0; pad <= 1; ++pad) {
+            CHECK(hipMemset(dbad, 0, 8));
+            if (pad)
+                hipLaunchKernelGGL(k_waw<1>, dim3(2048), dim3(256), 0, 0, dbad, 20000u, 4165u, 0u, 4165ull);
+            else
+                hipLaunchKernelGGL(k_waw<0>, dim3(2048), dim3(256), 0, 0, dbad, 20000u, 4165u, 0u, 4165ull);
+            CHECK(hipDeviceSynchronize());
+            unsigned long long hb = 0;
+            CHECK(hipMemcpy(&hb, dbad, 8, hipMemcpyDeviceToHost));
+            printf("k_waw pad %d: sequences %llu, SGPR pair not -1 after the s_cselect: %llu\n", pad,
+                   2048ull * 4 * 20000, hb);
+            fflush(stdout);
+        }
+    }
+    CHECK(hipFree(dbad));
+    for (int r = 0; r < reps; ++r) {
+        for (int v = 0; v <= 8; ++v) run(v);
+        run(1, 100);
+        run(1, 64);
+    }
     CHECK(hipFree(cnt));
     CHECK(hipFree(d));
     return 0;
