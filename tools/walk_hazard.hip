@@ -27,6 +27,12 @@
 //   else changed): whether the failures need waves of several workgroups
 //   sharing a SIMD
 //
+// k_rl: the walk's shape with nothing else -- a loop-carried wave-uniform
+// value (acc) that picks the next load address, takes lane m's loaded word
+// by v_readlane (SGPR, MODE 0) or by a ds_bpermute broadcast (VGPR, MODE 1),
+// and is updated by scalar (MODE 0) or vector (MODE 1) arithmetic; every wave
+// computes the same chain, checked against the host
+//
 // and a register-level test of that pattern (k_waw): v_mad_u64_u32 with its
 // carry-out in an SGPR pair, three VALU instructions, then an SALU write
 // (s_cselect_b64 -1) of the same pair, which must read back -1; P = the
@@ -200,6 +206,34 @@ __global__ __launch_bounds__(256) void k_waw(unsigned long long *bad, uint32_t i
     if (acc == 0x123456789ull) atomicAdd(bad, 1ull << 40);  // (keeps acc live)
 }
 
+template <int MODE>
+__global__ __launch_bounds__(256) void k_rl(const uint32_t *tab, uint32_t iters, uint32_t *out) {
+    const uint32_t j = threadIdx.x & 63u;
+    const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < iters; ++i) {
+        const uint32_t x = tab[(acc + j) & 4095u];
+        const uint32_t m = (acc >> 7) & 63u;
+        uint32_t r;
+        if (MODE == 0)
+            r = __builtin_amdgcn_readlane(x, __builtin_amdgcn_readfirstlane(m));
+        else
+            r = (uint32_t)__shfl((int)x, (int)m, 64);
+        acc = acc * 2654435761u + r + i;
+    }
+    if (j == 0) out[wave] = acc;
+}
+
+static uint32_t host_rl(const std::vector<uint32_t> &tab, uint32_t iters) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < iters; ++i) {
+        const uint32_t m = (acc >> 7) & 63u;
+        const uint32_t r = tab[(acc + m) & 4095u];
+        acc = acc * 2654435761u + r + i;
+    }
+    return acc;
+}
+
 static uint32_t host_walk(const uint8_t *h, uint64_t size) {
     uint64_t off = 0;
     uint32_t c = 0;
@@ -323,6 +357,41 @@ int main(int argc, char **argv) {
         }
     }
     CHECK(hipFree(dbad));
+    {
+        std::vector<uint32_t> tab(4096);
+        for (uint32_t i = 0; i < 4096; ++i) tab[i] = i * 2246822519u ^ (i >> 3) * 3266489917u;
+        uint32_t *dtab = nullptr, *dout = nullptr;
+        const uint32_t nblk = 2048, nwave = nblk * 4, iters = 20000;
+        CHECK(hipMalloc(&dtab, 4096 * 4));
+        CHECK(hipMalloc(&dout, nwave * 4));
+        CHECK(hipMemcpy(dtab, tab.data(), 4096 * 4, hipMemcpyHostToDevice));
+        CHECK(hipFuncSetAttribute((const void *)k_rl<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 100 << 10));
+        const uint32_t want = host_rl(tab, iters);
+        std::vector<uint32_t> got(nwave);
+        for (int r = 0; r < reps; ++r) {
+            for (int mode = 0; mode <= 2; ++mode) {  // 2: MODE 0 at one workgroup per CU
+                CHECK(hipMemset(dout, 0, nwave * 4));
+                if (mode == 1)
+                    hipLaunchKernelGGL(k_rl<1>, dim3(nblk), dim3(256), 0, 0, dtab, iters, dout);
+                else
+                    hipLaunchKernelGGL(k_rl<0>, dim3(nblk), dim3(256), mode == 2 ? 100 << 10 : 0, 0, dtab, iters, dout);
+                CHECK(hipDeviceSynchronize());
+                CHECK(hipMemcpy(got.data(), dout, nwave * 4, hipMemcpyDeviceToHost));
+                uint32_t bad = 0, first = ~0u;
+                for (uint32_t w = 0; w < nwave; ++w)
+                    if (got[w] != want) {
+                        ++bad;
+                        if (first == ~0u) first = w;
+                    }
+                printf("k_rl %s: waves %u, wrong %u (first wave %d)\n",
+                       mode == 0 ? "readlane/SGPR chain" : mode == 1 ? "bpermute/VGPR chain" : "readlane/SGPR chain, 1 workgroup per CU",
+                       nwave, bad, (int)first);
+                fflush(stdout);
+            }
+        }
+        CHECK(hipFree(dtab));
+        CHECK(hipFree(dout));
+    }
     for (int r = 0; r < reps; ++r) {
         for (int v = 0; v <= 8; ++v) run(v);
         run(1, 100);
