@@ -974,6 +974,11 @@ struct Queue {
     // Completion wakes exactly the job's own waiter (a futex on j->done): with
     // many IO threads a shared condition variable woke every waiter per launch,
     // and spinning waiters starved the dispatcher of CPU time.
+    // (A spinning waiter can see done == 1, return and free the job before
+    // the FUTEX_WAKE below runs.  The wake only hashes the address: on
+    // reused memory it at most wakes another job's waiter, which re-checks
+    // its word and sleeps again; on unmapped memory it fails with EFAULT.
+    // Neither writes memory, so the job is not touched after the store.)
     static void complete(crc32c_job *j, int rc) {
         j->rc = rc;
         j->done.store(1, std::memory_order_release);
