@@ -66,6 +66,13 @@ extern "C" {
                                  client_flags_t is 8 bytes, so ITEM_CFLAGS adds 8 to
                                  ITEM_ntotal instead of 4 (memcached.h:96-100, :149-152) */
 
+/* Longest span: 2 GiB - 64 KiB, twice the largest item memcached stores
+ * (ITEM_SIZE_MAX_UPPER_LIMIT, memcached.h:115).  A device span past it is not
+ * read (out[i] = 0, CRC32C_ERANGE; an item image claiming one is malformed);
+ * a fixed-length batch or a host batch with one is rejected (CRC32C_EINVAL;
+ * host spans are limited to 256 MiB each). */
+#define CRC32C_MAX_SPAN 0x7fff0000u
+
 /* A batch of byte spans inside one buffer.
  *   span i = [base + (offsets ? offsets[i] : i * stride),  + (lens ? lens[i] : len))
  *   out[i] = crc32c(crc_in ? crc_in[i] : 0, span i)

@@ -229,6 +229,12 @@ constexpr uint32_t kSpanCH = 32;
 constexpr uint32_t kRowBytes = 32 * kSpanCH;  // 1024
 constexpr uint32_t kBlockBytes = 4 * kRowBytes;  // 4096
 constexpr uint32_t kSegBytes = 64 * 1024;  // (16-256 KiB measured; 24-64 KiB alike)
+// Longest span (CRC32C_MAX_SPAN): a unit's grid offsets (eo, G - p, the block
+// count times 4 KiB) are 32-bit and signed, and a span that overlaps others
+// past the plan's capacity is one unit.  Twice the largest item memcached
+// stores (ITEM_SIZE_MAX_UPPER_LIMIT = 1 GiB, memcached.h:115).  Longer spans
+// are not read (out = 0, counted as out of range / malformed).
+constexpr uint32_t kMaxSpan = 0x7fff0000u;
 constexpr uint32_t kWhole = 0xffffffffu;      // unit segment index: the whole span
 // Pieces outside a span are read from a zeroed buffer; workgroup b reads the
 // 16 B at zero + 4 KiB * (b % 256), so the workgroups' zero reads spread over
@@ -532,7 +538,8 @@ __device__ __forceinline__ ItemDesc item_desc(const SpanArgs &a, uint64_t off, c
     // an item never crosses its write buffer (extstore.c:627-636), so a
     // header claiming otherwise is corrupt
     const bool in_region = a.region == 0 || off / a.region == (off + ntotal - 1) / a.region;
-    d.sane = hdr_ok && h.nkey != 0 && h.nbytes < 0x80000000u && off + ntotal <= a.base_bytes && in_region;
+    d.sane = hdr_ok && h.nkey != 0 && h.nbytes < 0x80000000u && ntotal - 32 <= kMaxSpan &&
+             off + ntotal <= a.base_bytes && in_region;
     d.p = a.base + off + 32;
     d.len = d.sane ? (uint32_t)(ntotal - 32) : 0u;
     return d;
@@ -545,7 +552,7 @@ __device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
         // a span outside [base, base + base_bytes) is not read (out = 0, counted)
         ItemDesc d;
         const uint32_t len = a.lens ? a.lens[i] : a.len;
-        d.sane = off <= a.base_bytes && len <= a.base_bytes - off;
+        d.sane = off <= a.base_bytes && len <= a.base_bytes - off && len <= kMaxSpan;
         d.p = a.base + (d.sane ? off : 0);
         d.len = d.sane ? len : 0u;
         d.aux = a.crc_in ? a.crc_in[i] : 0u;

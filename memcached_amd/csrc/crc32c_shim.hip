@@ -493,6 +493,7 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
 // here (the kernels read them unchecked).  Spans given by device offsets or
 // lengths are checked by the span kernels (out-of-range ones are not read).
 bool fixed_spans_fit(const crc32c_spans &s) {
+    if (!s.lens && s.len > mcrc_dev::kMaxSpan) return false;
     if (s.offsets || s.lens) return true;
     if (s.len > s.base_bytes) return false;
     if (s.n <= 1 || s.stride == 0) return true;

@@ -194,6 +194,42 @@ def test_very_long_spans(torch):
     np.testing.assert_array_equal(_u32(out), want)
 
 
+MAX_SPAN = 0x7FFF0000  # CRC32C_MAX_SPAN (include/crc32c_batch.h)
+
+
+def test_maximum_length_spans(torch):
+    """Spans at the length limit (2 GiB - 64 KiB) and just under it, past
+    2^31 - 2^20, overlapping so that the planner processes some as one unit
+    (the second span pass), next to a short and an empty span, in a buffer
+    past 2 GiB; a span one byte over the limit is not read: out 0 and
+    CRC32C_ERANGE, the others still exact."""
+    import ctypes
+    rng = np.random.default_rng(41)
+    size = (1 << 31) + 8192
+    host = np.frombuffer(rng.bytes(size), dtype=np.uint8)
+    offs = np.array([1, 7, (1 << 20) + 5, (1 << 31) + 100, 3, 2], dtype=np.uint64)
+    lens = np.array([MAX_SPAN, MAX_SPAN - 1, MAX_SPAN - (1 << 20) - 11, 4133, 0, MAX_SPAN + 1], dtype=np.uint32)
+    cin = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(host, offs[:-1], lens[:-1], cin[:-1])
+    d = _dev(torch, host)
+    d_offs, d_lens, d_cin = (_dev(torch, offs.view(np.int64)), _dev(torch, lens.view(np.int32)),
+                             _dev(torch, cin.view(np.int32)))
+    out = torch.empty(lens.size, dtype=torch.int32, device="cuda")
+    sp = _lib.Spans(d.data_ptr(), size, d_offs.data_ptr(), 0, d_lens.data_ptr(), 0, d_cin.data_ptr(),
+                    out.data_ptr(), lens.size)
+    assert _lib.lib.crc32c_batch(ctypes.byref(sp), _lib.CRC32C_DEVICE, None) == _lib.CRC32C_ERANGE
+    got = _u32(out)
+    np.testing.assert_array_equal(got[:-1], want)
+    assert got[-1] == 0
+    # without the oversize span the batch is clean
+    sp.n = lens.size - 1
+    assert _lib.lib.crc32c_batch(ctypes.byref(sp), _lib.CRC32C_DEVICE, None) == _lib.CRC32C_OK
+    np.testing.assert_array_equal(_u32(out)[:-1], want)
+    # a fixed-length batch over the limit is rejected before any launch
+    big = _lib.Spans(d.data_ptr(), size, None, 0, None, MAX_SPAN + 1, None, out.data_ptr(), 1)
+    assert _lib.lib.crc32c_batch(ctypes.byref(big), _lib.CRC32C_DEVICE, None) == _lib.CRC32C_EINVAL
+
+
 def test_overlapping_long_spans_whole_pass(torch):
     """Overlapping spans whose units exceed the planner's capacity are processed
     whole by the second pass; results stay exact."""
