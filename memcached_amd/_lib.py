@@ -26,6 +26,7 @@ CRC32C_DEVICE = 0x1
 CRC32C_ASYNC = 0x2
 CRC32C_ALIGNED16 = 0x4
 CRC32C_CFLAGS64 = 0x8
+CRC32C_MAX_SPAN = 0x7FFF0000  # longest span (include/crc32c_batch.h)
 
 # every symbol include/*.h declares (checked by tests/test_abi.py)
 EXPORTED = (

@@ -98,3 +98,14 @@ def test_no_gpu_means_enodev_not_a_cpu_fallback():
         assert call() == _lib.CRC32C_ENODEV, name
     assert _lib.lib.crc32c_host_alloc(4096) is None
     assert (out == 0).all()  # nothing was computed on the CPU
+
+
+def test_python_constants_match_the_header():
+    """Every #define CRC32C_* of include/crc32c_batch.h has the same value in
+    memcached_amd/_lib.py (the ctypes mirror the tests and bench use)."""
+    import re
+    hdr = open(os.path.join(ROOT, "include", "crc32c_batch.h")).read()
+    defs = dict(re.findall(r"#define (CRC32C_\w+) \(?(-?(?:0x)?[0-9a-fA-F]+)u?\)?", hdr))
+    assert len(defs) >= 12
+    for name, val in defs.items():
+        assert getattr(_lib, name) == int(val, 0), name

@@ -194,7 +194,7 @@ def test_very_long_spans(torch):
     np.testing.assert_array_equal(_u32(out), want)
 
 
-MAX_SPAN = 0x7FFF0000  # CRC32C_MAX_SPAN (include/crc32c_batch.h)
+MAX_SPAN = _lib.CRC32C_MAX_SPAN
 
 
 def test_maximum_length_spans(torch):
