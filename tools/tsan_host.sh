@@ -5,7 +5,7 @@
 #   bash tools/tsan_host.sh OUT     (after bash tools/build_tsan.sh here)
 source tools/gpu_guard.sh
 O=gpurun_out/${1:-tsan}; mkdir -p $O
-export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0"
+export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 suppressions=$PWD/tools/tsan_hip.supp"
 for n in queue_sim extstore_sim; do
   /opt/rocm/lib/llvm/bin/clang -O1 -g -fsanitize=thread -pthread -I include tests/integration/$n.c \
       -L ab -lmcrc32c_tsan -Wl,-rpath,$PWD/ab -o /tmp/tsan_$n || exit 1
