@@ -182,6 +182,31 @@ __device__ __forceinline__ uint32_t group_reduce32_span(uint32_t v, uint32_t lan
     return v;
 }
 
+// The pair / quad reductions on the span image (level 4 = level 3 twice, its
+// tables 16..19 hold the 4 KiB block fold).
+__device__ __forceinline__ uint32_t reduce_level4_span(uint32_t v, bool on) {
+    const uint32_t x = lane_down<4>(v);
+    if (on) v = apply_op<4>(kAuxTree + 12, apply_op<4>(kAuxTree + 12, v)) ^ x;
+    return v;
+}
+
+__device__ __forceinline__ uint32_t group_reduce32_pair_span(uint32_t a, uint32_t b, uint32_t lane) {
+    const uint32_t bs = __builtin_amdgcn_update_dpp(0u, b, 0x111, 0xf, 0xf, false);  // row_shr:1
+    uint32_t v = (lane & 1u) ? bs : a;
+    v = reduce_level<1>(v, (lane & 3u) < 2u);
+    v = reduce_level<2>(v, (lane & 7u) < 2u);
+    v = reduce_level<3>(v, (lane & 15u) < 2u);
+    return reduce_level4_span(v, (lane & 31u) < 2u);
+}
+
+__device__ __forceinline__ uint32_t group_reduce32_quad_span(uint32_t ab, uint32_t cd, uint32_t lane) {
+    const uint32_t cs = __builtin_amdgcn_update_dpp(0u, cd, 0x112, 0xf, 0xf, false);  // row_shr:2
+    uint32_t v = (lane & 2u) ? cs : ab;
+    v = reduce_level<2>(v, (lane & 7u) < 4u);
+    v = reduce_level<3>(v, (lane & 15u) < 4u);
+    return reduce_level4_span(v, (lane & 31u) < 4u);
+}
+
 // Copy a table image from global memory into this workgroup's LDS.
 // (A thread's loads are all issued before its LDS stores: one load, wait and
 // store per iteration made the 160 KiB copy ten dependent L2 round trips per

@@ -29,6 +29,17 @@ namespace mcrc_dev {
 // 16-B load of item bytes.  (Non-temporal loads measured no better for K1 and
 // 5-11 % worse for the span kernels.)
 __device__ __forceinline__ uint4 ld16(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
+// Global-memory byte and piece pointers.  k_items keeps its addresses in
+// these: derived from the kernel arguments through generic pointers, they
+// lost their address space to an optimizer freeze, and the flat loads that
+// result also count in lgkmcnt (every LDS wait of the chains then waits for
+// the block prefetch too).
+typedef const __attribute__((address_space(1))) uint8_t gbyte;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16(gbyte *p) {
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4 *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 __device__ __forceinline__ uint32_t dw4(const uint4 &v, int k) {
     return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
@@ -324,6 +335,10 @@ __device__ __forceinline__ Piece ld_piece(const uint8_t *p) {
     const uint4 v = *reinterpret_cast<const uint4 *>(p);
     return {v.x | ((uint64_t)v.y << 32), v.z | ((uint64_t)v.w << 32)};
 }
+__device__ __forceinline__ Piece ld_piece(gbyte *p) {
+    const uint4 v = ld16(p);
+    return {v.x | ((uint64_t)v.y << 32), v.z | ((uint64_t)v.w << 32)};
+}
 // Bytes moved s positions up (s <= 16), zeros shifted in.
 __device__ __forceinline__ Piece shl_bytes(Piece v, uint32_t s) {
     if (s >= 16) return {0, 0};
@@ -513,11 +528,12 @@ struct ItemHdr {
         return 48ull + nkey + 1 + nbytes + ((flags & 256u) ? cfl : 0) + ((flags & 2u) ? 8 : 0);
     }
 };
-__device__ __forceinline__ ItemHdr parse_hdr(const uint8_t *it) {
+template <typename BytePtr>
+__device__ __forceinline__ ItemHdr parse_hdr(BytePtr it) {
     // (pointer arithmetic, not an integer round trip: the loads stay global
     // loads instead of flat ones, which would also count in lgkmcnt)
     const uint32_t sh = (uint32_t)((uintptr_t)(it + 28) & 15u);  // 0..15
-    const uint8_t *q = it + 28 - sh;
+    const BytePtr q = it + 28 - sh;
     const bool two = sh + 13 >= 16;  // byte 41 lies in the next piece
     const Piece v0 = ld_piece(q), v1 = ld_piece(q + (two ? 16 : 0));
     const uint64_t w0 = v0.lo, w1 = v0.hi, w2 = two ? v1.lo : 0, w3 = two ? v1.hi : 0;
@@ -1310,6 +1326,269 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
         grp += 2 * gstep;
     }
     if (nsteps & 1) store(group_reduce32_dpp(lane_partial_x3s<32>(ra.d, c), lane), grp, ra.cur, li == 0);
+}
+
+// ===========================================================================
+// K5: one-block item images end to end (k_items)
+// ===========================================================================
+//
+// The planned path spends a pass per image before k_blocks (k_count: the
+// header, the head fragment and the tail piece) plus a select, an expansion
+// and k_final.  For images whose span is one 4 KiB block after a head
+// fragment of 4..kFragMax bytes (every 4165-B image of config 5) k_items
+// does it in one pass, in k_blocks' loop, with the per-image work done once
+// per image by one lane instead of once per step by 32 lanes:
+//   - epochs of 32 steps: at the start of an epoch each lane L of the wave
+//     takes the image of step L / 2, group L % 2 (the 64 images the wave
+//     checksums in that epoch): its offset, its header (ITEM_ntotal and the
+//     stored CRC, storage.c:567), its block start G = E + t - 4096, and the
+//     register r from ~0 over the head fragment [p, G) -- a per-lane
+//     slice-by-4 chain on this lane's copy of the replicated tables over at
+//     most nine 16-B pieces (bytes below p cleared, ~0 XORed in at p) --
+//     folded to C = M_4096(r) (^ M_t(~stored) for a verify);
+//   - each step, the two groups take G and t of their image from the epoch
+//     lanes (ds_bpermute), load the block, clear the t foreign bytes after E
+//     in lane 31's last piece, and run K1's chains;
+//   - four steps share one lane tree; lanes 0-3 of a group then hold
+//     R = M_t(raw of the span's block) of four images, XOR in their C
+//     (ds_bpermute) and give R ^ C = M_t(f), f the register after the whole
+//     span from ~0: a verify is good iff it is 0 (f == ~stored), a stamp
+//     writes {M_t(f), t} for k_fix.
+// Images that are sane but not of that shape go to a fallback list that the
+// planned path takes afterwards; malformed images are marked bad here.
+
+struct ItemsOut {
+    uint32_t *fb;   // items for the planned path (sane, not one block)
+    uint32_t *nfb;  // their count
+    uint2 *rt;      // MODE 2: per item {M_t(f), t | kRtFused}, {0, 0} if not fused
+};
+constexpr uint32_t kRtFused = 0x80000000u;
+
+// The fused shape: one block [Ea - 4096, Ea) after a head fragment of
+// 4..kFragMax bytes (vlen = len + t).
+__device__ __forceinline__ bool fused_vlen(uint32_t vlen) {
+    return vlen >= kBlockBytes + 4 && vlen - kBlockBytes <= kFragMax;
+}
+
+// The dword at A of the head fragment: bytes below p cleared (pa = p - A,
+// clamped to 0..4) and ~0 XORed into the bytes of [p, p + 4) it holds.
+__device__ __forceinline__ uint32_t head_dword(uint32_t v, int32_t pa) {
+    const uint32_t c = (uint32_t)min(max(pa, 0), 4), e = (uint32_t)min(max(pa + 4, 0), 4);
+    const uint32_t keep = c >= 4 ? 0u : ~0u << (8 * c), inj = e >= 4 ? ~0u : (1u << (8 * e)) - 1u;
+    return (v & keep) ^ (inj & keep);
+}
+// Bytes [16 - t, 16) of v cleared (t < 16).
+__device__ __forceinline__ uint4 clear_high(uint4 v, uint32_t t) {
+    const uint64_t mh = t >= 8 ? 0ull : ~0ull >> (8 * t);
+    const uint64_t ml = t <= 8 ? ~0ull : ~0ull >> (8 * (t - 8));
+    return make_uint4(v.x & (uint32_t)ml, v.y & (uint32_t)(ml >> 32), v.z & (uint32_t)mh, v.w & (uint32_t)(mh >> 32));
+}
+// M_t(v) for t < 16: t zero bytes through this lane's replicated slice-by-4
+// tables (t / 4 dword steps, then byte steps on T0).
+__device__ __forceinline__ uint32_t zeros_lds(uint32_t v, uint32_t t, const LaneCtx &c) {
+    for (uint32_t q = 0; q < (t >> 2); ++q) v = step4_next(v, 0u, c);
+    for (uint32_t r = 0; r < (t & 3u); ++r)
+        v = lds_ld(kAux4Bytes + 0x10000u + ((v & 0xffu) << 8) + 128u + c.lane4) ^ (v >> 8);
+    return v;
+}
+
+constexpr uint32_t kStFused = 0x10u, kStSane = 0x20u, kStValid = 0x40u;
+constexpr uint32_t kEpoch = 32;                                 // steps per epoch: 64 images per wave
+constexpr uint32_t kFragPieces = (kFragMax + 15) / 16 + 1;      // 16-B pieces of [floor16(p), G)
+
+struct ItemBuf {
+    ItemRegs<32, 32, 4> d;  // the block, rows 0..3
+    uint32_t st;            // its image: t | kStFused | kStSane | kStValid
+};
+
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restrict__ img, ItemsOut io) {
+    static_assert(MODE == 1 || MODE == 2, "item images: verify or stamp");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint64_t n = a.n;
+    const uint64_t waves = blockDim.x >> 6;
+    const uint64_t gstep = gridDim.x * waves;
+    const uint64_t ngroups = (n + 1) / 2;
+    const uint64_t grp0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
+    if ((uint64_t)blockIdx.x * waves >= ngroups) return;
+    load_tables(smem, img, kLdsImageK1Bytes);
+    if (grp0 >= ngroups) return;
+    const uint32_t lane = threadIdx.x & 63u, li = lane & 31u, g = lane >> 5;
+    LaneCtx c;
+    c.lane4 = li << 2;
+    c.lane4hi = c.lane4 | 0x10000u;
+    gbyte *const gb = (gbyte *)a.base;
+    gbyte *const gz = (gbyte *)(a.zero + (blockIdx.x % kZeroSlots) * (4096 / 16));
+    const uint32_t base_lo = (uint32_t)(uintptr_t)a.base;  // (for alignments: the offsets are from a.base)
+    const uint64_t nsteps = (ngroups - grp0 + gstep - 1) / gstep;
+    uint32_t nb = 0;  // bad (malformed or mismatching) images seen by this lane
+    // this lane's image of the epoch: block offset from a.base (lo, hi), status, C
+    uint32_t eglo = 0, eghi = 0, est = 0, ec = 0;
+
+    // The epoch starting at step e0 of this wave: lane L prepares the image
+    // of step e0 + L / 2, group L % 2.
+    auto prep = [&](uint64_t e0) {
+        const uint64_t gi = grp0 + (e0 + (lane >> 1)) * gstep;
+        const uint64_t item = gi * 2 + (lane & 1u);
+        const bool valid = e0 + (lane >> 1) < nsteps && item < n;
+        const uint64_t off = valid ? a.offsets[item] : 0;
+        const bool hdr_ok = valid && off + 48 <= a.base_bytes;
+        ItemHdr h{0u, 0u, 0u, 0u};
+        if (hdr_ok) h = parse_hdr(gb + off);
+        const ItemDesc it = item_desc(a, off, h, hdr_ok);
+        const uint32_t len = it.sane ? it.len : 0u;
+        const uint64_t po = off + 32;                               // span start (offset)
+        const uint32_t kh = (base_lo + (uint32_t)po) & 15u;         // its alignment
+        const uint32_t t = (0u - kh - len) & (kTailAlign - 1), vlen = len + t;  // tail_pad
+        const bool fused = it.sane && fused_vlen(vlen);
+        const uint64_t go = po + vlen - kBlockBytes;                // block start (offset)
+        // r = register from ~0 over [p, G): the pieces of [floor16(p), G),
+        // bytes below p cleared and ~0 injected at p (head_dword); a lane
+        // whose image is not fused reads zeros and keeps r = 0
+        const uint64_t pho = po - kh;
+        const uint32_t np16 = fused ? (uint32_t)(go - pho) >> 4 : 0u;
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kFragPieces; ++k) {
+            const uint4 v = ld16(k < np16 ? gb + pho + 16 * k : gz);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const int32_t pa = (int32_t)kh - (int32_t)(16 * k + 4 * j);
+                const uint32_t d = head_dword(w[j], pa);
+                const uint32_t nx = (k == 0 && j == 0) ? d : step4_next(x, d, c);
+                x = k < np16 ? nx : x;
+            }
+        }
+        x = np16 ? step4_next(x, 0u, c) : 0u;  // (past the last dword)
+        uint32_t cc = apply_op<4>(kAuxSpanFold, x);  // M_4096(r): the block follows
+        if (MODE == 1) cc ^= zeros_lds(~h.exptime, t, c);  // (R ^ C == 0 iff the stored CRC matches)
+        eglo = (uint32_t)go;
+        eghi = (uint32_t)(go >> 32);
+        est = t | (fused ? kStFused : 0u) | (it.sane ? kStSane : 0u) | (valid ? kStValid : 0u);
+        ec = fused ? cc : 0u;
+    };
+    // Loads of step s (< ns, else a repeat of the epoch's last step, whose
+    // result is not used) into b: its block and its status.
+    auto ld = [&](ItemBuf &b, uint32_t s, uint32_t ns) {
+        const int src = (int)(2 * min(s, ns - 1) + g);
+        const uint64_t lo = (uint32_t)__shfl((int)eglo, src, 64), hi = (uint32_t)__shfl((int)eghi, src, 64);
+        b.st = (uint32_t)__shfl((int)est, src, 64);
+        gbyte *blk = (b.st & kStFused) ? gb + (lo | (hi << 32)) : gz;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) b.d.d[r][q] = ld16(blk + r * 1024 + li * 32 + 16 * q);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto part0 = [&](ItemBuf &b) {
+        if (li == 31u) b.d.d[3][1] = clear_high(b.d.d[3][1], b.st & 15u);
+        return reduce_level<0>(lane_partial_x3s<32>(b.d, c), (lane & 1u) == 0u);
+    };
+    // Result R of step s of the epoch (lanes 0..3 of a group, s < ns): the
+    // image's verdict / stamp record.
+    auto finish = [&](uint32_t raw, uint64_t e0, uint32_t s, uint32_t ns, bool on) {
+        const int src = (int)(2 * min(s, ns - 1) + g);
+        const uint32_t cq = (uint32_t)__shfl((int)ec, src, 64), st = (uint32_t)__shfl((int)est, src, 64);
+        const uint64_t item = (grp0 + (e0 + s) * gstep) * 2 + g;
+        on = on && s < ns && (st & kStValid);
+        const bool fused = st & kStFused, sane = st & kStSane;
+        const bool fb = on && sane && !fused;
+        const uint32_t r = raw ^ cq;  // M_t(f) (verify: 0 iff good)
+        if (on) {
+            if (MODE == 1) {
+                if (fused || !sane) {
+                    const bool good = fused && r == 0u;
+                    a.ok[item] = good;
+                    nb += !good;
+                }
+            } else {
+                io.rt[item] = fused ? make_uint2(r, (st & 15u) | kRtFused) : make_uint2(0u, 0u);
+                if (!sane) {
+                    if (a.ok) a.ok[item] = 0;
+                    ++nb;
+                }
+            }
+        }
+        const uint64_t m = __ballot(fb);  // the fallback list: one atomic per wave with entries
+        if (m) {
+            const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+            uint32_t base = 0;
+            if (lane == first) base = atomicAdd(io.nfb, (uint32_t)__popcll(m));
+            base = __shfl(base, (int)first, 64);
+            if (fb) io.fb[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)item;
+        }
+    };
+    ItemBuf ra, rb;
+    for (uint64_t e0 = 0; e0 < nsteps; e0 += kEpoch) {
+        const uint32_t ns = (uint32_t)min((uint64_t)kEpoch, nsteps - e0);
+        prep(e0);
+        ld(ra, 0, ns);
+        uint32_t s = 0;
+        for (; s + 4 <= ns; s += 4) {
+            ld(rb, s + 1, ns);
+            const uint32_t va = part0(ra);
+            ld(ra, s + 2, ns);
+            const uint32_t vb = part0(rb);
+            const uint32_t vab = group_pair_level1(va, vb, lane);
+            ld(rb, s + 3, ns);
+            const uint32_t vc = part0(ra);
+            ld(ra, s + 4, ns);
+            const uint32_t vd = part0(rb);
+            const uint32_t raw = group_reduce32_quad_span(vab, group_pair_level1(vc, vd, lane), lane);
+            finish(raw, e0, s + (li & 3u), ns, li < 4);
+        }
+        for (; s + 2 <= ns; s += 2) {
+            ld(rb, s + 1, ns);
+            const uint32_t va = part0(ra);
+            ld(ra, s + 2, ns);
+            const uint32_t vb = part0(rb);
+            const uint32_t raw = group_reduce32_pair_span(va, vb, lane);
+            finish(raw, e0, s + (li & 1u), ns, li < 2);
+        }
+        if (s < ns) {
+            const uint32_t v = part0(ra);
+            // (part0 ran level 0; levels 1..4 of the span tree)
+            uint32_t r = reduce_level<1>(v, (lane & 3u) == 0u);
+            r = reduce_level<2>(r, (lane & 7u) == 0u);
+            r = reduce_level<3>(r, (lane & 15u) == 0u);
+            r = reduce_level4_span(r, (lane & 31u) == 0u);
+            finish(r, e0, s, ns, li == 0);
+        }
+    }
+    // one atomic per wave for the bad count
+    nb += __shfl_xor(nb, 1);
+    nb += __shfl_xor(nb, 2);
+    nb += __shfl_xor(nb, 4);
+    nb += __shfl_xor(nb, 8);
+    nb += __shfl_xor(nb, 16);
+    nb += __shfl_xor(nb, 32);
+    if (lane == 0 && nb) atomicAdd(a.nbad, (unsigned long long)nb);
+}
+
+// The stamps of k_items' one-block images, one thread per image: from
+// R = M_t(f), f the register after the span from ~0, the spill CRC is
+// ~M_{-t}(R) (storage.c:567), written into the image's exptime.
+__global__ void k_fix(SpanArgs a, const uint2 *rt) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint2 r = rt[i];
+        if (!(r.y & kRtFused)) continue;
+        const uint32_t crc = ~mulmodp_dev(r.x, a.xpow[kXpowInv + (r.y & 15u)]);
+        uint8_t *p = const_cast<uint8_t *>(a.base) + a.offsets[i] + 32;
+        __builtin_memcpy(p - 4, &crc, 4);
+        if (a.ok) a.ok[i] = 1;
+    }
+}
+
+// Fallback lists: gather the listed items' offsets / scatter their results.
+__global__ void k_gather_offs(const uint64_t *offsets, const uint32_t *idx, const uint32_t *nidx, uint64_t *out) {
+    const uint32_t nn = *nidx;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) out[i] = offsets[idx[i]];
+}
+__global__ void k_scatter_ok(const uint8_t *ok_in, const uint32_t *idx, const uint32_t *nidx, uint8_t *ok) {
+    const uint32_t nn = *nidx;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) ok[idx[i]] = ok_in[i];
 }
 
 // Chained CRC over an iov list (the chunked-item read verify of

@@ -81,6 +81,7 @@ struct Device {
     // images): zero between calls, kept so by the kernel's last workgroup
     unsigned long long *small_nbad = nullptr;
     uint32_t *small_done = nullptr;
+    uint32_t *nfb = nullptr, *hfb = nullptr;  // k_items' fallback count (device, pinned twin)
     hipStream_t stream = nullptr, copy = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};  // host-batch pipeline slots
@@ -124,7 +125,7 @@ struct Device {
     struct Scratch {
         void *p = nullptr;
         size_t bytes = 0;
-    } scratch[8];
+    } scratch[12];
     void *grow(int slot, size_t bytes) {
         Scratch &s = scratch[slot];
         if (s.bytes < bytes) {
@@ -160,7 +161,10 @@ struct Device {
         return true;
     }
 };
-enum { kScrWalkCnt, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage, kScrItemOffs, kScrItemOut };
+enum {
+    kScrWalkCnt, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage, kScrItemOffs, kScrItemOut,
+    kScrFb, kScrFbOffs, kScrFbOk, kScrRt
+};
 enum { kPinStage, kPinOffs, kPinOk, kPinCrc };
 
 std::mutex g_dev_mu;
@@ -246,6 +250,8 @@ int init_device(Device &d, int id) {
     HIP_OK(hipMalloc(&d.small_nbad, 16));
     HIP_OK(hipMemset(d.small_nbad, 0, 16));
     d.small_done = reinterpret_cast<uint32_t *>(d.small_nbad + 1);
+    HIP_OK(hipMalloc(&d.nfb, sizeof(uint32_t)));
+    HIP_OK(hipHostMalloc(&d.hfb, sizeof(uint32_t), hipHostMallocDefault));
     HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&d.ev0));
@@ -266,6 +272,8 @@ int init_device(Device &d, int id) {
         (const void *)mcrc_dev::k_blocks<false, true>,
         (const void *)mcrc_dev::k_blocks<true, true>,
         (const void *)mcrc_dev::k_blocks<true, false>,
+        (const void *)mcrc_dev::k_items<1>,
+        (const void *)mcrc_dev::k_items<2>,
     };
     for (const void *k : k160)
         HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImageK1Bytes));
@@ -355,6 +363,15 @@ bool one_block_len(uint32_t len) {
         if (!(drop ? vlen - g1o == mcrc_dev::kBlockBytes : len && x == mcrc_dev::kBlockBytes)) return false;
     }
     return true;
+}
+
+// Item images whose average size is that of a fused span's image (ntotal
+// 4132..4256 B: 4 KiB values, configs 1 and 5) go through K5; other mixes
+// through the planned path (K5 would send most of them to its fallback).
+bool items_fused(const mcrc_dev::SpanArgs &a) {
+    if (a.n < 4096) return false;
+    const uint64_t avg = a.base_bytes / a.n;
+    return avg >= mcrc_dev::kBlockBytes + 36 && avg <= mcrc_dev::kBlockBytes + 32 + mcrc_dev::kFragMax + 32;
 }
 
 // Batches of at most g_small_max spans take the single-launch k_small
@@ -484,6 +501,52 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     w.nunits = nwhole;
     spans(w, d.cus);
     hipLaunchKernelGGL((mcrc_dev::k_final<MODE, true>), dim3(gf), dim3(256), 0, st, u, d.irec);
+    HIP_OK(hipGetLastError());
+    return CRC32C_OK;
+}
+
+// K5 over the item images of a (MODE 1 verify, MODE 2 stamp; device memory,
+// a.nbad zeroed by the caller): k_items (+ k_fix for stamps), then the
+// planned path over the images it listed as not one block.  Synchronous: the
+// length of that list is read back.
+template <int MODE>
+int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
+    const uint64_t n = a.n;
+    if (n >= 0xffffffffull) return CRC32C_EINVAL;
+    mcrc_dev::ItemsOut io{};
+    io.fb = (uint32_t *)d.grow(kScrFb, n * 4);
+    io.nfb = d.nfb;
+    if (MODE == 2) io.rt = (uint2 *)d.grow(kScrRt, n * 8);
+    if (!io.fb || (MODE == 2 && !io.rt)) return CRC32C_ENOMEM;
+    HIP_OK(hipMemsetAsync(d.nfb, 0, 4, st));
+    hipLaunchKernelGGL((mcrc_dev::k_items<MODE>), dim3(grid_for(d, n)), dim3(1024),
+                       mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
+    if (MODE == 2)
+        hipLaunchKernelGGL(mcrc_dev::k_fix, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256),
+                           0, st, a, (const uint2 *)io.rt);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(d.hfb, d.nfb, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const uint64_t nfb = *d.hfb;
+    if (nfb == 0) return CRC32C_OK;
+    uint64_t *fo = (uint64_t *)d.grow(kScrFbOffs, nfb * 8);
+    uint8_t *fok = (uint8_t *)d.grow(kScrFbOk, nfb);
+    if (!fo || !fok) return CRC32C_ENOMEM;
+    const unsigned g = (unsigned)std::min<uint64_t>((nfb + 255) / 256, 1024);
+    hipLaunchKernelGGL(mcrc_dev::k_gather_offs, dim3(g), dim3(256), 0, st, a.offsets, (const uint32_t *)io.fb,
+                       (const uint32_t *)d.nfb, fo);
+    mcrc_dev::SpanArgs f = a;
+    const bool want_ok = MODE == 1 || a.ok;
+    f.offsets = fo;
+    f.n = nfb;
+    f.ok = want_ok ? fok : nullptr;
+    Path path;
+    path.small = takes_small<MODE>(f);
+    int rc = launch_units<MODE>(d, f, st, path);
+    if (rc) return rc;
+    if (want_ok)
+        hipLaunchKernelGGL(mcrc_dev::k_scatter_ok, dim3(g), dim3(256), 0, st, (const uint8_t *)fok,
+                           (const uint32_t *)io.fb, (const uint32_t *)d.nfb, a.ok);
     HIP_OK(hipGetLastError());
     return CRC32C_OK;
 }
@@ -816,9 +879,12 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
         a.ok = ok;
         a.out = nullptr;  // stamp: write into the images
         path.host_counted = path.small;
+        // K5 for synchronous calls over one-block images (it reads back the
+        // length of its fallback list)
+        const bool k5 = !path.small && !((flags & CRC32C_ASYNC) && !nbad) && items_fused(a);
         d->acquire(st);
         if (!path.host_counted) (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
-        rc = launch_units<MODE>(*d, a, st, path);
+        rc = k5 ? launch_items<MODE>(*d, a, st) : launch_units<MODE>(*d, a, st, path);
         if (!rc && !path.host_counted)
             rc = hipMemcpyAsync(d->hbad, d->nbad, sizeof(unsigned long long), hipMemcpyDeviceToHost, st) == hipSuccess
                      ? CRC32C_OK
@@ -1375,7 +1441,8 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     // entries k_count would make (the headers are read once more, not twice)
     Path path;
     path.small = takes_small<1>(a);
-    path.counted = !path.small;
+    const bool k5 = !path.small && items_fused(a);  // (then the walk writes offsets only)
+    path.counted = !path.small && !k5;
     if (path.counted) {
         rc = ensure_plan(*d, total, plan_cap(a));
         if (rc) return rc;
@@ -1389,7 +1456,7 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     wo.fast = path.counted ? d->fast : nullptr;
     HIP_OK(hipMemsetAsync(d->nbad, 0, 2 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(mcrc_dev::k_walk<true>, dim3(gw), bw, 0, st, a, nw, wo);
-    rc = launch_units<1>(*d, a, st, path);
+    rc = k5 ? launch_items<1>(*d, a, st) : launch_units<1>(*d, a, st, path);
     if (rc) return rc;
     HIP_OK(hipMemcpyAsync(d->hbad, d->nbad, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     const uint64_t k = std::min<uint64_t>(cap, total);

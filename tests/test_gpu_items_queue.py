@@ -300,3 +300,123 @@ def test_two_ranks_device_batch_path(torch):
         p.join(timeout=240)
         assert p.exitcode == 0
     assert q.get(timeout=10) is True
+
+
+# ---------------------------------------------------------------------------
+# One-block spans; K5 (k_items): one-block item images end to end
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("length", [4100, 4133, 4171, 4209])
+def test_k5_fixed_length_spans(torch, length):
+    """Batches of equal spans of 4100..4209 bytes (one block after a head
+    fragment at every alignment: k_blocks + k_final): by stride and by
+    offsets at every alignment, with and without initial CRCs, and a span
+    outside the buffer (ERANGE, not read)."""
+    rng = np.random.default_rng(length)
+    n = 9000  # past the single-launch path's 8192
+    stride = length + 29
+    buf = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+    d = torch.from_numpy(buf).cuda()
+    offs = (np.arange(n, dtype=np.uint64) * stride + 7).astype(np.uint64)
+    want = oracle.batch(buf, offs, np.full(n, length, np.uint64))
+    # by stride (base + 7: every alignment occurs)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    sp = _lib.Spans(d.data_ptr() + 7, buf.size - 7, None, stride, None, length, None, out.data_ptr(), n)
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp), _lib.CRC32C_DEVICE, None))
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+    # by offsets, shuffled, with crc_in
+    perm = rng.permutation(n)
+    cin = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    got = mc.batch(d, offsets=torch.from_numpy(offs[perm].view(np.int64)).cuda(), length=length,
+                   crc_in=torch.from_numpy(cin.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32),
+                                  oracle.batch(buf, offs[perm], np.full(n, length, np.uint64), cin))
+    # one span past the end: out 0, CRC32C_ERANGE, the others exact
+    bad = offs.copy()
+    bad[123] = buf.size - length + 1
+    out2 = torch.empty(n, dtype=torch.int32, device="cuda")
+    o2 = torch.from_numpy(bad.view(np.int64)).cuda()
+    sp2 = _lib.Spans(d.data_ptr(), buf.size, o2.data_ptr(), 0, None, length, None, out2.data_ptr(), n)
+    assert _lib.lib.crc32c_batch(ctypes.byref(sp2), _lib.CRC32C_DEVICE, None) == _lib.CRC32C_ERANGE
+    g2 = out2.cpu().numpy().view(np.uint32)
+    assert g2[123] == 0
+    np.testing.assert_array_equal(np.delete(g2, 123), np.delete(want, 123))
+
+
+def _expected_verdicts(buf, offs, wbuf):
+    """The oracle's verdict per image, as the library defines it: the header
+    parses to a span inside the buffer and inside the image's wbuf, nkey != 0,
+    and the stored exptime equals the spill CRC of that span."""
+    ok = np.zeros(offs.size, np.uint8)
+    for i, o in enumerate(offs.tolist()):
+        if o + 48 > buf.size or buf[o + 41] == 0:
+            continue
+        nbytes = int.from_bytes(bytes(buf[o + 32:o + 36]), "little")
+        if nbytes >= 1 << 31:
+            continue
+        nt = layout.ntotal_of(buf, o)
+        if o + nt > buf.size or o // wbuf != (o + nt - 1) // wbuf:
+            continue
+        stored = int.from_bytes(bytes(buf[o + 28:o + 32]), "little")
+        ok[i] = stored == oracle.item_crc(buf, o)
+    return ok
+
+
+def test_k5_verify_stamp_and_walk_with_fallback(torch):
+    """Pages of 4165-B images (the K5 shape) with every kind of damage: a
+    flipped length bit (some images then leave the one-block shape -- the
+    fallback list and the planned path -- and some their wbuf -- malformed),
+    a zeroed key length, a flipped data bit, and a few images of other sizes.
+    Verify by offsets and by the device walk, and stamp: exact against the
+    oracle, image by image."""
+    rng = np.random.default_rng(55)
+    wbuf = 1 << 20
+    n = 6000
+    vals = [4096 if i % 50 else int(rng.integers(200, 9000)) for i in range(n)]
+    items = [layout.make_item(b"key%07d" % i, rng.integers(0, 256, v, dtype=np.uint8).tobytes(), cas=i + 1)
+             for i, v in enumerate(vals)]
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    soffs, slens = layout.spans_of(buf, offs)
+    layout.store_crcs(buf, offs, oracle.batch(buf, soffs, slens))
+    clean = buf.copy()
+    victims = rng.choice(n, 300, replace=False)
+    for k, v in enumerate(victims.tolist()):
+        o = int(offs[v])
+        if k % 3 == 0:
+            buf[o + 32 + int(rng.integers(0, 2))] ^= 1 << int(rng.integers(0, 8))  # length bit
+        elif k % 3 == 1:
+            buf[int(soffs[v]) + int(rng.integers(16, slens[v]))] ^= 1 << int(rng.integers(0, 8))  # data bit
+        else:
+            buf[o + 40] ^= 0x40  # slabs_clsid: in the span, header stays sane
+    buf[int(offs[17]) + 41] = 0  # a zeroed key length: malformed
+    want = _expected_verdicts(buf, offs, wbuf)
+    d = torch.from_numpy(buf).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    for _ in range(2):
+        ok, nbad = mc.verify_items(d, do, region_bytes=wbuf)
+        np.testing.assert_array_equal(ok.cpu().numpy(), want)
+        assert nbad == int((want == 0).sum())
+    # the device walk of the same pages: stops where a damaged length sends it
+    # (storage.c:950-960); compared with a host walk + the oracle
+    w_offs, w_ok, w_bad = mc.verify_pages(d, wbuf)
+    h_offs = []
+    for w0 in range(0, buf.size, wbuf):
+        o = w0
+        while o + 48 <= min(w0 + wbuf, buf.size) and buf[o + 41] != 0:
+            h_offs.append(o)
+            nbytes = int.from_bytes(bytes(buf[o + 32:o + 36]), "little")  # (unsigned, as the kernels)
+            o += layout.ntotal_of(buf, o) - int(np.int32(np.uint32(nbytes))) + nbytes
+    h_offs = np.asarray(h_offs, np.uint64)
+    np.testing.assert_array_equal(w_offs.cpu().numpy().astype(np.uint64), h_offs)
+    hw = _expected_verdicts(buf, h_offs, wbuf)
+    np.testing.assert_array_equal(w_ok.cpu().numpy(), hw)
+    assert w_bad == int((hw == 0).sum())
+    # stamp the clean pages with exptime zeroed: every image gets its spill CRC
+    z = clean.copy()
+    layout.store_crcs(z, offs, np.zeros(n, np.uint32))
+    dz = torch.from_numpy(z).cuda()
+    ok, nbad = mc.stamp_items(dz, do, region_bytes=wbuf)
+    torch.cuda.synchronize()
+    assert nbad == 0 and bool(ok.all())
+    np.testing.assert_array_equal(dz.cpu().numpy(), clean)

@@ -1,7 +1,8 @@
 """HBM traffic per batch of the span workloads (config 3, config 5) from
 rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs (tools/s3_traffic.sh): every
 library kernel of the batch, summed per batch (one k_count dispatch per
-batch), against the algorithmic bytes.  gfx950 correction as tools/traffic.py
+batch; config 5 with K5: one k_items dispatch per batch), against the
+algorithmic bytes.  gfx950 correction as tools/traffic.py
 (FETCH_SIZE x 2, KiB).
     python tools/traffic_spans.py FETCH_DIR WRITE_DIR ALGO_BYTES OUT"""
 import csv
@@ -27,7 +28,7 @@ def per_kernel(d, counter):
 
 f, fc = per_kernel(sys.argv[1], "FETCH_SIZE")
 w, _ = per_kernel(sys.argv[2], "WRITE_SIZE")
-batches = max(v for k, v in fc.items() if k.startswith("k_count"))
+batches = max(v for k, v in fc.items() if k.startswith(("k_count", "k_items")))
 algo = float(sys.argv[3])
 rec = {"batches": batches, "algorithmic_bytes_per_batch": algo, "per_kernel_bytes_per_batch": {}}
 total = 0.0
