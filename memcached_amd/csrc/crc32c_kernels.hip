@@ -1366,16 +1366,18 @@ constexpr uint32_t kRtFused = 0x80000000u;
 
 // The fused shape: one block [Ea - 4096, Ea) after a head fragment of
 // 4..kFragMax bytes (vlen = len + t).
-__device__ __forceinline__ bool fused_vlen(uint32_t vlen) {
+__host__ __device__ __forceinline__ bool fused_vlen(uint32_t vlen) {
     return vlen >= kBlockBytes + 4 && vlen - kBlockBytes <= kFragMax;
 }
 
-// The dword at A of the head fragment: bytes below p cleared (pa = p - A,
-// clamped to 0..4) and ~0 XORed into the bytes of [p, p + 4) it holds.
-__device__ __forceinline__ uint32_t head_dword(uint32_t v, int32_t pa) {
-    const uint32_t c = (uint32_t)min(max(pa, 0), 4), e = (uint32_t)min(max(pa + 4, 0), 4);
-    const uint32_t keep = c >= 4 ? 0u : ~0u << (8 * c), inj = e >= 4 ? ~0u : (1u << (8 * e)) - 1u;
-    return (v & keep) ^ (inj & keep);
+// The dword at A of the head fragment: bytes below p cleared (pa = p - A)
+// and the four bytes of inj (~c for an initial CRC c: a register seeded with
+// ~c, crc32c.c:166) XORed into the bytes of [p, p + 4) it holds.
+__device__ __forceinline__ uint32_t head_dword(uint32_t v, int32_t pa, uint32_t inj) {
+    if (pa >= 4) return 0u;
+    if (pa >= 0) return (v & (~0u << (8 * pa))) ^ (inj << (8 * pa));
+    if (pa > -4) return v ^ (inj >> (8 * -pa));
+    return v;
 }
 // Bytes [16 - t, 16) of v cleared (t < 16).
 __device__ __forceinline__ uint4 clear_high(uint4 v, uint32_t t) {
@@ -1401,9 +1403,11 @@ struct ItemBuf {
     uint32_t st;            // its image: t | kStFused | kStSane | kStValid
 };
 
-template <int MODE>
+template <int MODE, bool OFFS>
 __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restrict__ img, ItemsOut io) {
-    static_assert(MODE == 1 || MODE == 2, "item images: verify or stamp");
+    // MODE 0: equal spans of a.len bytes by offsets (OFFS) or stride (every
+    // one of the fused shape: the shim checks a.len at every alignment),
+    // MODE 1/2: item images (verify / stamp) by offsets
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint64_t n = a.n;
     const uint64_t waves = blockDim.x >> 6;
@@ -1426,47 +1430,77 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
     uint32_t eglo = 0, eghi = 0, est = 0, ec = 0;
 
     // The epoch starting at step e0 of this wave: lane L prepares the image
-    // of step e0 + L / 2, group L % 2.
-    auto prep = [&](uint64_t e0) {
-        const uint64_t gi = grp0 + (e0 + (lane >> 1)) * gstep;
-        const uint64_t item = gi * 2 + (lane & 1u);
-        const bool valid = e0 + (lane >> 1) < nsteps && item < n;
-        const uint64_t off = valid ? a.offsets[item] : 0;
-        const bool hdr_ok = valid && off + 48 <= a.base_bytes;
+    // of step e0 + L / 2, group L % 2, in three stages so that the first
+    // block's loads overlap the fragment chain: prep_head (offset -- loaded
+    // during the previous epoch -- header, shape, block address), the
+    // fragment's piece loads, then (after the epoch's first block load is
+    // issued) prep_chain.
+    auto item_of = [&](uint64_t e0) -> uint64_t { return (grp0 + (e0 + (lane >> 1)) * gstep) * 2 + (lane & 1u); };
+    auto valid_of = [&](uint64_t e0) { return e0 + (lane >> 1) < nsteps && item_of(e0) < n; };
+    auto off_of = [&](uint64_t e0) -> uint64_t {
+        // (offsets or stride is a template choice: a load on one side of a
+        // branch leaves the waitcnt pass a merged state that waits for it)
+        return valid_of(e0) ? (OFFS ? a.offsets[item_of(e0)] : item_of(e0) * a.stride) : 0;
+    };
+    uint64_t noff = off_of(0);  // the offset of this lane's image in the next epoch
+    uint32_t ncin = MODE == 0 && a.crc_in && valid_of(0) ? a.crc_in[item_of(0)] : 0u;
+    // stage state
+    uint32_t p_kh = 0, p_t = 0, p_np16 = 0, p_inj = ~0u, p_stored = 0;
+    uint64_t p_pho = 0;
+    uint4 pc[kFragPieces];
+    auto prep_head = [&](uint64_t e0) {
+        const bool valid = valid_of(e0);
+        const uint64_t off = noff;
         ItemHdr h{0u, 0u, 0u, 0u};
-        if (hdr_ok) h = parse_hdr(gb + off);
-        const ItemDesc it = item_desc(a, off, h, hdr_ok);
+        ItemDesc it{a.base, 0u, 0u, false};
+        p_inj = ~0u;  // ~c: the register's initial value, XORed in at p
+        if (MODE == 0) {
+            it.sane = valid && off <= a.base_bytes && a.len <= a.base_bytes - off;
+            it.len = a.len;
+            if (a.crc_in) p_inj = ~ncin;
+        } else {
+            const bool hdr_ok = valid && off + 48 <= a.base_bytes;
+            if (hdr_ok) h = parse_hdr(gb + off);
+            it = item_desc(a, off, h, hdr_ok);
+        }
+        p_stored = h.exptime;
         const uint32_t len = it.sane ? it.len : 0u;
-        const uint64_t po = off + 32;                               // span start (offset)
-        const uint32_t kh = (base_lo + (uint32_t)po) & 15u;         // its alignment
-        const uint32_t t = (0u - kh - len) & (kTailAlign - 1), vlen = len + t;  // tail_pad
+        const uint64_t po = MODE == 0 ? off : off + 32;             // span start (offset)
+        p_kh = (base_lo + (uint32_t)po) & 15u;                     // its alignment
+        p_t = (0u - p_kh - len) & (kTailAlign - 1);                 // tail_pad
+        const uint32_t vlen = len + p_t;
         const bool fused = it.sane && fused_vlen(vlen);
         const uint64_t go = po + vlen - kBlockBytes;                // block start (offset)
-        // r = register from ~0 over [p, G): the pieces of [floor16(p), G),
-        // bytes below p cleared and ~0 injected at p (head_dword); a lane
-        // whose image is not fused reads zeros and keeps r = 0
-        const uint64_t pho = po - kh;
-        const uint32_t np16 = fused ? (uint32_t)(go - pho) >> 4 : 0u;
+        p_pho = po - p_kh;
+        p_np16 = fused ? (uint32_t)(go - p_pho) >> 4 : 0u;
+        eglo = (uint32_t)go;
+        eghi = (uint32_t)(go >> 32);
+        est = p_t | (fused ? kStFused : 0u) | (it.sane ? kStSane : 0u) | (valid ? kStValid : 0u);
+    };
+    // the fragment's pieces (a lane whose span is not fused reads zeros)
+    auto prep_pieces = [&]() {
+#pragma unroll
+        for (uint32_t k = 0; k < kFragPieces; ++k) pc[k] = ld16(k < p_np16 ? gb + p_pho + 16 * k : gz);
+    };
+    // r = register from ~c over [p, G): the pieces of [floor16(p), G), bytes
+    // below p cleared and ~c injected at p (head_dword); C = M_4096(r)
+    auto prep_chain = [&]() {
         uint32_t x = 0;
 #pragma unroll
         for (uint32_t k = 0; k < kFragPieces; ++k) {
-            const uint4 v = ld16(k < np16 ? gb + pho + 16 * k : gz);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t w[4] = {pc[k].x, pc[k].y, pc[k].z, pc[k].w};
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j) {
-                const int32_t pa = (int32_t)kh - (int32_t)(16 * k + 4 * j);
-                const uint32_t d = head_dword(w[j], pa);
+                const int32_t pa = (int32_t)p_kh - (int32_t)(16 * k + 4 * j);
+                const uint32_t d = head_dword(w[j], pa, p_inj);
                 const uint32_t nx = (k == 0 && j == 0) ? d : step4_next(x, d, c);
-                x = k < np16 ? nx : x;
+                x = k < p_np16 ? nx : x;
             }
         }
-        x = np16 ? step4_next(x, 0u, c) : 0u;  // (past the last dword)
+        x = p_np16 ? step4_next(x, 0u, c) : 0u;  // (past the last dword)
         uint32_t cc = apply_op<4>(kAuxSpanFold, x);  // M_4096(r): the block follows
-        if (MODE == 1) cc ^= zeros_lds(~h.exptime, t, c);  // (R ^ C == 0 iff the stored CRC matches)
-        eglo = (uint32_t)go;
-        eghi = (uint32_t)(go >> 32);
-        est = t | (fused ? kStFused : 0u) | (it.sane ? kStSane : 0u) | (valid ? kStValid : 0u);
-        ec = fused ? cc : 0u;
+        if (MODE == 1) cc ^= zeros_lds(~p_stored, p_t, c);  // (R ^ C == 0 iff the stored CRC matches)
+        ec = p_np16 ? cc : 0u;
     };
     // Loads of step s (< ns, else a repeat of the epoch's last step, whose
     // result is not used) into b: its block and its status.
@@ -1493,10 +1527,13 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
         const uint64_t item = (grp0 + (e0 + s) * gstep) * 2 + g;
         on = on && s < ns && (st & kStValid);
         const bool fused = st & kStFused, sane = st & kStSane;
-        const bool fb = on && sane && !fused;
+        const bool fb = MODE != 0 && on && sane && !fused;
         const uint32_t r = raw ^ cq;  // M_t(f) (verify: 0 iff good)
         if (on) {
-            if (MODE == 1) {
+            if (MODE == 0) {
+                io.rt[item] = fused ? make_uint2(r, (st & 15u) | kRtFused) : make_uint2(0u, 0u);
+                nb += !sane;  // (out of the buffer: not read, out 0, counted)
+            } else if (MODE == 1) {
                 if (fused || !sane) {
                     const bool good = fused && r == 0u;
                     a.ok[item] = good;
@@ -1510,20 +1547,27 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
                 }
             }
         }
-        const uint64_t m = __ballot(fb);  // the fallback list: one atomic per wave with entries
-        if (m) {
-            const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-            uint32_t base = 0;
-            if (lane == first) base = atomicAdd(io.nfb, (uint32_t)__popcll(m));
-            base = __shfl(base, (int)first, 64);
-            if (fb) io.fb[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)item;
+        if (MODE != 0) {
+            const uint64_t m = __ballot(fb);  // the fallback list: one atomic per wave with entries
+            if (m) {
+                const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+                uint32_t base = 0;
+                if (lane == first) base = atomicAdd(io.nfb, (uint32_t)__popcll(m));
+                base = __shfl(base, (int)first, 64);
+                if (fb) io.fb[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)item;
+            }
         }
     };
     ItemBuf ra, rb;
     for (uint64_t e0 = 0; e0 < nsteps; e0 += kEpoch) {
         const uint32_t ns = (uint32_t)min((uint64_t)kEpoch, nsteps - e0);
-        prep(e0);
+        prep_head(e0);
+        prep_pieces();
+        // the next epoch's offsets (and initial CRCs), consumed one epoch later
+        noff = off_of(e0 + kEpoch);
+        if (MODE == 0) ncin = a.crc_in && valid_of(e0 + kEpoch) ? a.crc_in[item_of(e0 + kEpoch)] : 0u;
         ld(ra, 0, ns);
+        prep_chain();
         uint32_t s = 0;
         for (; s + 4 <= ns; s += 4) {
             ld(rb, s + 1, ns);
@@ -1566,18 +1610,23 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
     if (lane == 0 && nb) atomicAdd(a.nbad, (unsigned long long)nb);
 }
 
-// The stamps of k_items' one-block images, one thread per image: from
-// R = M_t(f), f the register after the span from ~0, the spill CRC is
-// ~M_{-t}(R) (storage.c:567), written into the image's exptime.
+// The last step of k_items, one thread per span: from R = M_t(f), f the
+// register after the span from ~c, the CRC is ~M_{-t}(R): MODE 0 writes it
+// to out[] (0 for a span outside the buffer), MODE 2 stamps it into the
+// image's exptime as the spill CRC (storage.c:567).
+template <int MODE>
 __global__ void k_fix(SpanArgs a, const uint2 *rt) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint2 r = rt[i];
-        if (!(r.y & kRtFused)) continue;
         const uint32_t crc = ~mulmodp_dev(r.x, a.xpow[kXpowInv + (r.y & 15u)]);
-        uint8_t *p = const_cast<uint8_t *>(a.base) + a.offsets[i] + 32;
-        __builtin_memcpy(p - 4, &crc, 4);
-        if (a.ok) a.ok[i] = 1;
+        if (MODE == 0) {
+            a.out[i] = (r.y & kRtFused) ? crc : 0u;
+        } else if (r.y & kRtFused) {
+            uint8_t *p = const_cast<uint8_t *>(a.base) + a.offsets[i] + 32;
+            __builtin_memcpy(p - 4, &crc, 4);
+            if (a.ok) a.ok[i] = 1;
+        }
     }
 }
 

@@ -272,8 +272,10 @@ int init_device(Device &d, int id) {
         (const void *)mcrc_dev::k_blocks<false, true>,
         (const void *)mcrc_dev::k_blocks<true, true>,
         (const void *)mcrc_dev::k_blocks<true, false>,
-        (const void *)mcrc_dev::k_items<1>,
-        (const void *)mcrc_dev::k_items<2>,
+        (const void *)mcrc_dev::k_items<0, true>,
+        (const void *)mcrc_dev::k_items<0, false>,
+        (const void *)mcrc_dev::k_items<1, true>,
+        (const void *)mcrc_dev::k_items<2, true>,
     };
     for (const void *k : k160)
         HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImageK1Bytes));
@@ -365,6 +367,17 @@ bool one_block_len(uint32_t len) {
     return true;
 }
 
+// Every span of `len` bytes, at any alignment, is one block after a head
+// fragment of 4..kFragMax bytes (mcrc_dev::fused_vlen): k_items takes the
+// batch whole (configs 2r: 4133-B spans).
+bool fused_len(uint32_t len) {
+    for (uint32_t kh = 0; kh < 16; ++kh) {
+        const uint32_t vlen = len + ((0u - kh - len) & (mcrc_dev::kTailAlign - 1));
+        if (!mcrc_dev::fused_vlen(vlen)) return false;
+    }
+    return true;
+}
+
 // Item images whose average size is that of a fused span's image (ntotal
 // 4132..4256 B: 4 KiB values, configs 1 and 5) go through K5; other mixes
 // through the planned path (K5 would send most of them to its fallback).
@@ -449,6 +462,20 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
         }
         return launch_small<MODE>(d, a, st);
     }
+    if (identity && fused_len(a.len) && n < 0xffffffffull) {  // K5: one block after a head fragment
+        mcrc_dev::ItemsOut io{};
+        io.rt = (uint2 *)d.grow(kScrRt, n * 8);
+        if (!io.rt) return CRC32C_ENOMEM;
+        if (a.offsets)
+            hipLaunchKernelGGL((mcrc_dev::k_items<0, true>), dim3(grid_for(d, n)), dim3(1024),
+                               mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
+        else
+            hipLaunchKernelGGL((mcrc_dev::k_items<0, false>), dim3(grid_for(d, n)), dim3(1024),
+                               mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
+        hipLaunchKernelGGL((mcrc_dev::k_fix<0>), dim3(gf), dim3(256), 0, st, a, (const uint2 *)io.rt);
+        HIP_OK(hipGetLastError());
+        return CRC32C_OK;
+    }
     if (identity) {
         // (spans of at most kWholeMax - 15 bytes are all their threads' in k_final)
         if (a.len + mcrc_dev::kTailAlign - 1 > mcrc_dev::kWholeMax) {
@@ -519,10 +546,10 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     if (MODE == 2) io.rt = (uint2 *)d.grow(kScrRt, n * 8);
     if (!io.fb || (MODE == 2 && !io.rt)) return CRC32C_ENOMEM;
     HIP_OK(hipMemsetAsync(d.nfb, 0, 4, st));
-    hipLaunchKernelGGL((mcrc_dev::k_items<MODE>), dim3(grid_for(d, n)), dim3(1024),
+    hipLaunchKernelGGL((mcrc_dev::k_items<MODE, true>), dim3(grid_for(d, n)), dim3(1024),
                        mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
     if (MODE == 2)
-        hipLaunchKernelGGL(mcrc_dev::k_fix, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256),
+        hipLaunchKernelGGL((mcrc_dev::k_fix<2>), dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256),
                            0, st, a, (const uint2 *)io.rt);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(d.hfb, d.nfb, 4, hipMemcpyDeviceToHost, st));
