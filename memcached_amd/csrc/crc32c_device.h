@@ -44,6 +44,15 @@ __device__ __forceinline__ uint32_t lds_ld(uint32_t byte_addr) {
     return *reinterpret_cast<lds_cu32 *>(static_cast<uintptr_t>(byte_addr));
 }
 
+// VGPR allocation floor.  The walk experiment (tools/walk_hazard.hip,
+// DESIGN.md section 3) found a kernel whose identical instruction stream walks
+// wrongly when allocated 24 VGPRs with several workgroups per CU and exactly
+// at 32, 40 and 48 (and at 24 with one workgroup per CU).  Every kernel that
+// runs several workgroups per CU therefore allocates at least 32 VGPRs; on
+// gfx950 that costs no occupancy (8 waves per SIMD up to 64 VGPRs).
+// tests/test_kernel_resources.py checks the built code object.
+#define MCRC_VGPR_FLOOR() asm volatile("" ::: "v31")
+
 // Per-lane constants for table addressing.
 struct LaneCtx {
     uint32_t lane4;    // (lane & 31) << 2

@@ -953,6 +953,7 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
 
 template <int MODE>
 __global__ void k_count(SpanArgs a, uint32_t *nunit, uint4 *irec, uint8_t *fast) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     __shared__ __attribute__((aligned(16))) uint32_t s8[kTab8Dwords];
     const Tab8 t8 = load_tab8(s8, a.tab8);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
@@ -975,6 +976,7 @@ __device__ __forceinline__ uint32_t first_seg(const uint8_t *p, uint32_t len, ui
 __global__ void k_expand(const uint8_t *base, const uint32_t *nunit, const uint32_t *prefix, const uint4 *irec,
                          uint64_t n, UnitRec *units, uint64_t cap, uint32_t *nvalid, UnitRec *whole,
                          uint32_t *nwhole, uint32_t *big, uint32_t *nbig) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t p0 = prefix[i], ns = nunit[i];
@@ -999,6 +1001,7 @@ __global__ void k_expand(const uint8_t *base, const uint32_t *nunit, const uint3
 
 __global__ void k_expand_big(const uint8_t *base, const uint32_t *nunit, const uint32_t *prefix, const uint4 *irec,
                              UnitRec *units, const uint32_t *big, const uint32_t *nbig) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     const uint32_t nb = *nbig;
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint32_t i = big[b];
@@ -1037,6 +1040,7 @@ __device__ __forceinline__ void count_bad(unsigned long long *nbad, uint32_t nb)
 //   one unit per span (MODE 0, no plan): R = out[i], Z computed here.
 template <int MODE, bool UNITS>
 __global__ void k_final(SpanArgs a, const uint4 *irec) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     __shared__ __attribute__((aligned(16))) uint32_t s8[UNITS ? 1 : kTab8Dwords];
     Tab8 t8{s8};
     if (!UNITS) t8 = load_tab8(s8, a.tab8);
@@ -1616,6 +1620,7 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
 // image's exptime as the spill CRC (storage.c:567).
 template <int MODE>
 __global__ void k_fix(SpanArgs a, const uint2 *rt) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint2 r = rt[i];
@@ -1632,10 +1637,12 @@ __global__ void k_fix(SpanArgs a, const uint2 *rt) {
 
 // Fallback lists: gather the listed items' offsets / scatter their results.
 __global__ void k_gather_offs(const uint64_t *offsets, const uint32_t *idx, const uint32_t *nidx, uint64_t *out) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     const uint32_t nn = *nidx;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) out[i] = offsets[idx[i]];
 }
 __global__ void k_scatter_ok(const uint8_t *ok_in, const uint32_t *idx, const uint32_t *nidx, uint8_t *ok) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     const uint32_t nn = *nidx;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) ok[idx[i]] = ok_in[i];
 }
@@ -1648,6 +1655,7 @@ __global__ void k_scatter_ok(const uint8_t *ok_in, const uint32_t *idx, const ui
 // One thread per chain.
 __global__ void k_chain(const uint32_t *iov_crc, const uint32_t *lens, uint32_t len, const uint64_t *first,
                         uint64_t nchains, uint32_t *out, const uint32_t *xpow) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nchains;
          c += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t acc = 0;
@@ -1694,6 +1702,7 @@ struct WalkOut {
 // entries xpow, tab8, span_acc.
 template <bool EMIT>
 __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t nw, WalkOut out) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     __shared__ __attribute__((aligned(16))) uint32_t s8[EMIT ? kTab8Dwords : 1];
     Tab8 t8{s8};
     const bool plan = EMIT && out.irec;

@@ -1,0 +1,63 @@
+"""The gfx950 code object inside libmcrc32c.so: register allocation of every
+product kernel (no GPU needed).
+
+The page-walk experiment (tools/walk_hazard.hip) found a
+kernel whose identical instruction stream walks wrongly when it is allocated
+24 VGPRs and several workgroups share a CU, and exactly with 32, 40 or 48.
+Every mcrc_dev kernel therefore allocates at least 32 VGPRs
+(MCRC_VGPR_FLOOR, crc32c_device.h); this test reads the allocation back from
+the built library's kernel metadata.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from memcached_amd import _lib
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _code_object(tmp_path):
+    lib = _lib.LIB_PATH
+    if not os.path.exists(lib):
+        pytest.skip("libmcrc32c.so not built")
+    bundler = os.path.join(LLVM, "clang-offload-bundler")
+    if not (shutil.which("objcopy") and os.path.exists(bundler)):
+        pytest.skip("objcopy / clang-offload-bundler not available")
+    fat = tmp_path / "fatbin.bin"
+    co = tmp_path / "gfx950.co"
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, str(fat)], check=True)
+    subprocess.run([bundler, "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    return co
+
+
+def _kernels(co):
+    notes = subprocess.run([os.path.join(LLVM, "llvm-readobj"), "--notes", str(co)], check=True,
+                           capture_output=True, text=True).stdout
+    out = {}
+    for blk in notes.split("  - .agpr_count")[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+        vgpr = int(re.search(r"\.vgpr_count:\s+(\d+)", blk).group(1))
+        agpr = int(blk.split()[1])
+        lds = int(re.search(r"\.group_segment_fixed_size:\s+(\d+)", blk).group(1))
+        out[name] = (vgpr, agpr, lds)
+    return out
+
+
+def test_every_product_kernel_allocates_at_least_32_vgprs(tmp_path):
+    ks = {n: v for n, v in _kernels(_code_object(tmp_path)).items() if "mcrc_dev" in n}
+    # every kernel of crc32c_kernels.hip is in the library
+    for k in ("k_fixed", "k_spans", "k_count", "k_expand", "k_expand_big", "k_final", "k_small", "k_blocks",
+              "k_items", "k_fix", "k_gather_offs", "k_scatter_ok", "k_chain", "k_walk"):
+        assert any(re.search(rf"\d{k}E", n) or re.search(rf"\d{k}I", n) for n in ks), k
+    low = {n: v for n, (v, a, _) in ks.items() if ((v + 7) // 8) * 8 < 32}
+    assert not low, f"kernels allocating fewer than 32 VGPRs: {low}"
+    # and no kernel pays occupancy for the floor: the small per-thread kernels
+    # stay within 64 VGPRs (8 waves per SIMD)
+    for n, (v, a, lds) in ks.items():
+        if any(f"{len(k)}{k}" in n for k in ("k_fix", "k_gather_offs", "k_scatter_ok", "k_chain")):
+            assert v <= 64, (n, v)

@@ -19,6 +19,8 @@
 //   V6  V5 with 5 more wait states before each v_readlane
 //   V7  V1 recording, per wbuf, its first four round trips (off, s, m, k,
 //       lane 0's header fields) for the post-mortem of a wrong wbuf
+//   V9, V10, V11  V1 with its VGPR allocation raised from 24 to 32, 40 and 48
+//       (an asm clobber of v31 / v39 / v47; the code is V1's)
 //   V8  V1 with the lane's header offset in 32-bit arithmetic (off + j * s
 //       < 4 GiB in a wbuf): no v_mad_u64_u32, whose carry-out SGPR pair the
 //       compiler reuses 5 instructions later for an s_cselect in V1-V7
@@ -63,6 +65,11 @@ __device__ uint32_t *g_trace;  // V7: [wbuf][round 0..3][8 dwords]
 
 template <int V>
 __global__ __launch_bounds__(64 * kWalkWaves) void k_count_v(SpanArgs a, uint64_t nw, uint32_t *cnt) {
+    // V9-V11: V1 with its VGPR allocation raised from 24 to 32 / 40 / 48
+    // (a clobber of the top register; nothing else changes)
+    if (V == 9) asm volatile("" ::: "v31");
+    if (V == 10) asm volatile("" ::: "v39");
+    if (V == 11) asm volatile("" ::: "v47");
     const uint32_t j = threadIdx.x & 63u;
     const uint64_t wbuf = a.region;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -206,8 +213,12 @@ __global__ __launch_bounds__(256) void k_waw(unsigned long long *bad, uint32_t i
     if (acc == 0x123456789ull) atomicAdd(bad, 1ull << 40);  // (keeps acc live)
 }
 
-template <int MODE>
+template <int MODE, int CLOB = 0>
 __global__ __launch_bounds__(256) void k_rl(const uint32_t *tab, uint32_t iters, uint32_t *out) {
+    // CLOB: the VGPR allocation raised to 16 / 24 / 32 (a clobber of the top register)
+    if (CLOB == 16) asm volatile("" ::: "v15");
+    if (CLOB == 24) asm volatile("" ::: "v23");
+    if (CLOB == 32) asm volatile("" ::: "v31");
     const uint32_t j = threadIdx.x & 63u;
     const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
     uint32_t acc = 0;
@@ -298,7 +309,10 @@ int main(int argc, char **argv) {
             case 5: hipLaunchKernelGGL(k_count_v<5>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
             case 6: hipLaunchKernelGGL(k_count_v<6>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
             case 7: hipLaunchKernelGGL(k_count_v<7>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
-            default: hipLaunchKernelGGL(k_count_v<8>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 8: hipLaunchKernelGGL(k_count_v<8>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 9: hipLaunchKernelGGL(k_count_v<9>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            case 10: hipLaunchKernelGGL(k_count_v<10>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
+            default: hipLaunchKernelGGL(k_count_v<11>, dim3(gw), dim3(64 * kWalkWaves), 0, 0, a, nwb, cnt); break;
         }
         CHECK(hipDeviceSynchronize());
         CHECK(hipMemcpy(got.data(), cnt, nwb * 4, hipMemcpyDeviceToHost));
@@ -337,6 +351,37 @@ int main(int argc, char **argv) {
         }
         fflush(stdout);
     };
+    if (argc > 3 && !strcmp(argv[3], "vgpr")) {  // only the VGPR-allocation variants
+        for (int r = 0; r < reps; ++r)
+            for (int v : {0, 1, 9, 10, 11}) run(v);
+        run(1, 100);
+        // k_rl (readlane/SGPR chain) at 8 (its own count), 16, 24 and 32 VGPRs
+        std::vector<uint32_t> tab(4096);
+        for (uint32_t i = 0; i < 4096; ++i) tab[i] = i * 2246822519u ^ (i >> 3) * 3266489917u;
+        uint32_t *dtab = nullptr, *dout = nullptr;
+        const uint32_t nblk = 2048, nwave = nblk * 4, iters = 20000;
+        CHECK(hipMalloc(&dtab, 4096 * 4));
+        CHECK(hipMalloc(&dout, nwave * 4));
+        CHECK(hipMemcpy(dtab, tab.data(), 4096 * 4, hipMemcpyHostToDevice));
+        const uint32_t want = host_rl(tab, iters);
+        std::vector<uint32_t> gotw(nwave);
+        for (int r = 0; r < reps; ++r)
+            for (int cl : {0, 16, 24, 32}) {
+                CHECK(hipMemset(dout, 0, nwave * 4));
+                if (cl == 0) hipLaunchKernelGGL((k_rl<0, 0>), dim3(nblk), dim3(256), 0, 0, dtab, iters, dout);
+                if (cl == 16) hipLaunchKernelGGL((k_rl<0, 16>), dim3(nblk), dim3(256), 0, 0, dtab, iters, dout);
+                if (cl == 24) hipLaunchKernelGGL((k_rl<0, 24>), dim3(nblk), dim3(256), 0, 0, dtab, iters, dout);
+                if (cl == 32) hipLaunchKernelGGL((k_rl<0, 32>), dim3(nblk), dim3(256), 0, 0, dtab, iters, dout);
+                CHECK(hipDeviceSynchronize());
+                CHECK(hipMemcpy(gotw.data(), dout, nwave * 4, hipMemcpyDeviceToHost));
+                uint32_t bad = 0;
+                for (uint32_t w = 0; w < nwave; ++w) bad += gotw[w] != want;
+                printf("k_rl readlane/SGPR chain, VGPRs %s: waves %u, wrong %u\n",
+                       cl == 0 ? "8 (own)" : cl == 16 ? "16" : cl == 24 ? "24" : "32", nwave, bad);
+                fflush(stdout);
+            }
+        return 0;
+    }
     // the register-level test: 2048 blocks of 4 waves (8 per CU), 20000
     // sequences per wave, with and without the pad
     unsigned long long *dbad = nullptr;
@@ -393,7 +438,7 @@ int main(int argc, char **argv) {
         CHECK(hipFree(dout));
     }
     for (int r = 0; r < reps; ++r) {
-        for (int v = 0; v <= 8; ++v) run(v);
+        for (int v = 0; v <= 11; ++v) run(v);
         run(1, 100);
         run(1, 64);
     }
