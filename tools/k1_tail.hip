@@ -12,6 +12,7 @@
 //   /tmp/k1_tail [REPS]
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <vector>
@@ -329,6 +330,27 @@ int main(int argc, char **argv) {
             hipLaunchKernelGGL((k_fixed_dyn<true, 16>), dim3(grid), dim3(1024), kLdsImageK1Bytes, 0, base, stride, n,
                                img, o, st, ctl);
     };
+    if (argc > 2 && !strcmp(argv[2], "block")) {  // K1 with fewer waves per CU (one workgroup per CU)
+        for (int i = 0; i < 300; ++i) run(1ull << 20, 0, out, cus);
+        for (int round = 0; round < 3; ++round)
+            for (int bs : {1024, 896, 768, 640, 512}) {
+                std::vector<double> ms;
+                for (int r = 0; r < reps; ++r) {
+                    CHECK(hipEventRecord(e0));
+                    hipLaunchKernelGGL(k_fixed<false>, dim3(cus), dim3(bs), kLdsImageK1Bytes, 0, base, stride,
+                                       1ull << 20, img, (const uint32_t *)nullptr, out2);
+                    CHECK(hipEventRecord(e1));
+                    CHECK(hipEventSynchronize(e1));
+                    float x;
+                    CHECK(hipEventElapsedTime(&x, e0, e1));
+                    ms.push_back(x);
+                }
+                printf("round %d block %4d: median %.4f ms min %.4f max %.4f\n", round, bs, pct(ms, .5), pct(ms, 0),
+                       pct(ms, 1));
+                fflush(stdout);
+            }
+        return 0;
+    }
     // exactness of the dynamic split (and of its head reset across launches):
     // sizes around the chunk and pool edges, small grids
     {
