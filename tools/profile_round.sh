@@ -16,4 +16,5 @@ run 60 python tools/traffic.py $O/fetch $O/write $O/traffic.json > /dev/null
 run 300 rocprofv3 --kernel-trace --stats -d $O/kt_c3 -o c3 --output-format csv -- python3 bench.py --workload config3 --steps 3 --warmup 1 > $O/kt_c3.json 2> $O/kt_c3.err
 run 300 rocprofv3 --kernel-trace --stats -d $O/kt_c5 -o c5 --output-format csv -- python3 bench.py --workload config5 --pages 300 --steps 3 --warmup 1 > $O/kt_c5.json 2> $O/kt_c5.err
 run 300 rocprofv3 --kernel-trace --stats -d $O/kt_c2r -o c2r --output-format csv -- python3 bench.py --workload config2r --steps 5 --warmup 1 > $O/kt_c2r.json 2> $O/kt_c2r.err
+run 300 rocprofv3 --kernel-trace --stats -d $O/kt_c5k -o c5k --output-format csv -- python3 bench.py --workload config5 --pages 1000 --steps 3 --warmup 1 > $O/kt_c5k.json 2> $O/kt_c5k.err
 echo done
