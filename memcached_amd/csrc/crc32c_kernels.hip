@@ -1357,14 +1357,15 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
 //     R = M_t(raw of the span's block) of four images, XOR in their C
 //     (ds_bpermute) and give R ^ C = M_t(f), f the register after the whole
 //     span from ~0: a verify is good iff it is 0 (f == ~stored), a stamp
-//     writes {M_t(f), t} for k_fix.
+//     writes {M_t(f), t} for k_fix, and a MODE 0 span's value goes back to
+//     its epoch lane, which stores ~M_{-t}(M_t(f)) at the end of the epoch.
 // Images that are sane but not of that shape go to a fallback list that the
 // planned path takes afterwards; malformed images are marked bad here.
 
 struct ItemsOut {
     uint32_t *fb;   // items for the planned path (sane, not one block)
     uint32_t *nfb;  // their count
-    uint2 *rt;      // MODE 2: per item {M_t(f), t | kRtFused}, {0, 0} if not fused
+    uint2 *rt;      // MODE 2: per item {M_t(f), t | kRtFused}, {0, 0} if not fused (for k_fix)
 };
 constexpr uint32_t kRtFused = 0x80000000u;
 
@@ -1446,6 +1447,9 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
         // branch leaves the waitcnt pass a merged state that waits for it)
         return valid_of(e0) ? (OFFS ? a.offsets[item_of(e0)] : item_of(e0) * a.stride) : 0;
     };
+    // MODE 0: x^(-8t), t < 16, lane-distributed (lane j holds t = j & 15);
+    // loaded before the first epoch's loads, so their waits retire it
+    const uint32_t xinv = MODE == 0 ? a.xpow[kXpowInv + (lane & 15u)] : 0u;
     uint64_t noff = off_of(0);  // the offset of this lane's image in the next epoch
     uint32_t ncin = MODE == 0 && a.crc_in && valid_of(0) ? a.crc_in[item_of(0)] : 0u;
     // stage state
@@ -1525,7 +1529,7 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
     };
     // Result R of step s of the epoch (lanes 0..3 of a group, s < ns): the
     // image's verdict / stamp record.
-    auto finish = [&](uint32_t raw, uint64_t e0, uint32_t s, uint32_t ns, bool on) {
+    auto finish = [&](uint32_t raw, uint64_t e0, uint32_t s, uint32_t ns, bool on) -> uint32_t {
         const int src = (int)(2 * min(s, ns - 1) + g);
         const uint32_t cq = (uint32_t)__shfl((int)ec, src, 64), st = (uint32_t)__shfl((int)est, src, 64);
         const uint64_t item = (grp0 + (e0 + s) * gstep) * 2 + g;
@@ -1535,8 +1539,7 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
         const uint32_t r = raw ^ cq;  // M_t(f) (verify: 0 iff good)
         if (on) {
             if (MODE == 0) {
-                io.rt[item] = fused ? make_uint2(r, (st & 15u) | kRtFused) : make_uint2(0u, 0u);
-                nb += !sane;  // (out of the buffer: not read, out 0, counted)
+                nb += !sane;  // (out of the buffer: not read, out 0, counted; the CRC: emit_epoch)
             } else if (MODE == 1) {
                 if (fused || !sane) {
                     const bool good = fused && r == 0u;
@@ -1561,6 +1564,23 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
                 if (fb) io.fb[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)item;
             }
         }
+        return r;
+    };
+    // MODE 0: the epoch lanes collect R ^ C = M_t(f) of their images from the
+    // lanes that finished them (steps s0 .. s0 + cnt - 1 in lanes 0 .. cnt - 1
+    // of each group), and at the end of the epoch each lane stores the CRC of
+    // its image, ~M_{-t}(M_t(f)) -- one multiply per image by one lane, in
+    // place of a pass over the batch (k_fix).
+    uint32_t er = 0;
+    auto collect = [&](uint32_t r, uint32_t s0, uint32_t cnt) {
+        const uint32_t sl = lane >> 1;
+        const int src = (int)((lane & 1u) * 32u + (sl - s0));
+        const uint32_t v = (uint32_t)__shfl((int)r, sl - s0 < cnt ? src : 0, 64);
+        er = sl - s0 < cnt ? v : er;
+    };
+    auto emit_epoch = [&](uint64_t e0) {
+        const uint32_t xt = (uint32_t)__shfl((int)xinv, (int)(est & 15u), 64);
+        if (valid_of(e0)) a.out[item_of(e0)] = (est & kStFused) ? ~mulmodp_dev(er, xt) : 0u;
     };
     ItemBuf ra, rb;
     for (uint64_t e0 = 0; e0 < nsteps; e0 += kEpoch) {
@@ -1584,7 +1604,8 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
             ld(ra, s + 4, ns);
             const uint32_t vd = part0(rb);
             const uint32_t raw = group_reduce32_quad_span(vab, group_pair_level1(vc, vd, lane), lane);
-            finish(raw, e0, s + (li & 3u), ns, li < 4);
+            const uint32_t r = finish(raw, e0, s + (li & 3u), ns, li < 4);
+            if (MODE == 0) collect(r, s, 4);
         }
         for (; s + 2 <= ns; s += 2) {
             ld(rb, s + 1, ns);
@@ -1592,7 +1613,8 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
             ld(ra, s + 2, ns);
             const uint32_t vb = part0(rb);
             const uint32_t raw = group_reduce32_pair_span(va, vb, lane);
-            finish(raw, e0, s + (li & 1u), ns, li < 2);
+            const uint32_t r = finish(raw, e0, s + (li & 1u), ns, li < 2);
+            if (MODE == 0) collect(r, s, 2);
         }
         if (s < ns) {
             const uint32_t v = part0(ra);
@@ -1601,8 +1623,10 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
             r = reduce_level<2>(r, (lane & 7u) == 0u);
             r = reduce_level<3>(r, (lane & 15u) == 0u);
             r = reduce_level4_span(r, (lane & 31u) == 0u);
-            finish(r, e0, s, ns, li == 0);
+            r = finish(r, e0, s, ns, li == 0);
+            if (MODE == 0) collect(r, s, 1);
         }
+        if (MODE == 0) emit_epoch(e0);
     }
     // one atomic per wave for the bad count
     nb += __shfl_xor(nb, 1);
@@ -1614,20 +1638,19 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
     if (lane == 0 && nb) atomicAdd(a.nbad, (unsigned long long)nb);
 }
 
-// The last step of k_items, one thread per span: from R = M_t(f), f the
-// register after the span from ~c, the CRC is ~M_{-t}(R): MODE 0 writes it
-// to out[] (0 for a span outside the buffer), MODE 2 stamps it into the
-// image's exptime as the spill CRC (storage.c:567).
-template <int MODE>
+// The last step of a K5 stamp (MODE 2), one thread per image: from R = M_t(f),
+// f the register after the span from ~0, the CRC is ~M_{-t}(R), stamped into
+// the image's exptime as the spill CRC (storage.c:567).  A separate pass:
+// within k_items an image's stamp could race with another wave's read of the
+// same bytes when images overlap.  (MODE 0 spans get their CRC from the epoch
+// lanes of k_items itself.)
 __global__ void k_fix(SpanArgs a, const uint2 *rt) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint2 r = rt[i];
-        const uint32_t crc = ~mulmodp_dev(r.x, a.xpow[kXpowInv + (r.y & 15u)]);
-        if (MODE == 0) {
-            a.out[i] = (r.y & kRtFused) ? crc : 0u;
-        } else if (r.y & kRtFused) {
+        if (r.y & kRtFused) {
+            const uint32_t crc = ~mulmodp_dev(r.x, a.xpow[kXpowInv + (r.y & 15u)]);
             uint8_t *p = const_cast<uint8_t *>(a.base) + a.offsets[i] + 32;
             __builtin_memcpy(p - 4, &crc, 4);
             if (a.ok) a.ok[i] = 1;

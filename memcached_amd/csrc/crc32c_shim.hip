@@ -463,16 +463,13 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
         return launch_small<MODE>(d, a, st);
     }
     if (identity && fused_len(a.len) && n < 0xffffffffull) {  // K5: one block after a head fragment
-        mcrc_dev::ItemsOut io{};
-        io.rt = (uint2 *)d.grow(kScrRt, n * 8);
-        if (!io.rt) return CRC32C_ENOMEM;
+        mcrc_dev::ItemsOut io{};  // (MODE 0: k_items stores every CRC itself)
         if (a.offsets)
             hipLaunchKernelGGL((mcrc_dev::k_items<0, true>), dim3(grid_for(d, n)), dim3(1024),
                                mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
         else
             hipLaunchKernelGGL((mcrc_dev::k_items<0, false>), dim3(grid_for(d, n)), dim3(1024),
                                mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
-        hipLaunchKernelGGL((mcrc_dev::k_fix<0>), dim3(gf), dim3(256), 0, st, a, (const uint2 *)io.rt);
         HIP_OK(hipGetLastError());
         return CRC32C_OK;
     }
@@ -549,7 +546,7 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     hipLaunchKernelGGL((mcrc_dev::k_items<MODE, true>), dim3(grid_for(d, n)), dim3(1024),
                        mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
     if (MODE == 2)
-        hipLaunchKernelGGL((mcrc_dev::k_fix<2>), dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256),
+        hipLaunchKernelGGL(mcrc_dev::k_fix, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256),
                            0, st, a, (const uint2 *)io.rt);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(d.hfb, d.nfb, 4, hipMemcpyDeviceToHost, st));
