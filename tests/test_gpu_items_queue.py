@@ -344,6 +344,34 @@ def test_k5_fixed_length_spans(torch, length):
     np.testing.assert_array_equal(np.delete(g2, 123), np.delete(want, 123))
 
 
+@pytest.mark.parametrize("n", [300001, 262144 * 2 + 8192 * 3 + 5])
+def test_k5_spans_full_epochs(torch, n):
+    """K5 MODE 0 over enough equal spans that every wave runs whole 32-step
+    epochs plus a partial one (quad, pair and single tails): every CRC goes
+    from the lanes that finish four images per quad back to the images' epoch
+    lanes, which store it (no k_fix pass).  The config 2 variant's shape
+    (4133-B spans at stride 4165, start +32), by stride, and by shuffled
+    offsets with initial CRCs; every CRC against the oracle."""
+    length, stride = 4133, 4165
+    g = torch.Generator(device="cuda").manual_seed(n)
+    d = torch.randint(0, 256, (n * stride + 64,), dtype=torch.uint8, device="cuda", generator=g)
+    buf = d.cpu().numpy()
+    offs = np.arange(n, dtype=np.uint64) * stride + 32
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    sp = _lib.Spans(d.data_ptr() + 32, d.numel() - 32, None, stride, None, length, None, out.data_ptr(), n)
+    _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp), _lib.CRC32C_DEVICE, None))
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32),
+                                  oracle.batch(buf, offs, np.full(n, length, np.uint64)))
+    rng = np.random.default_rng(n)
+    perm = rng.permutation(n)
+    cin = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    got = mc.batch(d, offsets=torch.from_numpy(offs[perm].view(np.int64)).cuda(), length=length,
+                   crc_in=torch.from_numpy(cin.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32),
+                                  oracle.batch(buf, offs[perm], np.full(n, length, np.uint64), cin))
+
+
 def _expected_verdicts(buf, offs, wbuf):
     """The oracle's verdict per image, as the library defines it: the header
     parses to a span inside the buffer and inside the image's wbuf, nkey != 0,
