@@ -372,6 +372,40 @@ def test_k5_spans_full_epochs(torch, n):
                                   oracle.batch(buf, offs[perm], np.full(n, length, np.uint64), cin))
 
 
+def test_k5_stamp_and_verify_full_epochs(torch):
+    """K5 stamps (MODE 2: k_items then k_fix) and verifies (MODE 1) over
+    enough 4165-B images for whole 32-step epochs and a partial one: every
+    stamped exptime equals the oracle's spill CRC (storage.c:567), the verify
+    of the stamped images passes them all, and one flipped byte per 1000
+    images is caught exactly."""
+    n, nt = 300007, 4165
+    g = torch.Generator(device="cuda").manual_seed(11)
+    d = torch.randint(0, 256, (n * nt + 64,), dtype=torch.uint8, device="cuda", generator=g)
+    im = d[:n * nt].view(n, nt)
+    # memcached.h:613-636 header: nbytes 4098 (4096 + CRLF), it_flags ITEM_CAS,
+    # nkey 10 -> ITEM_ntotal = 48 + 10 + 1 + 4098 + 8 = 4165; exptime zeroed
+    im[:, 28:32] = 0
+    im[:, 32:36] = torch.tensor([4098 & 255, 4098 >> 8, 0, 0], dtype=torch.uint8, device="cuda")
+    im[:, 38:40] = torch.tensor([2, 0], dtype=torch.uint8, device="cuda")
+    im[:, 41] = 10
+    offs = np.arange(n, dtype=np.uint64) * nt
+    doffs = torch.from_numpy(offs.view(np.int64)).cuda()
+    before = d.cpu().numpy()
+    want = oracle.batch(before, offs + 32, np.full(n, nt - 32, np.uint64))
+    ok, nbad = mc.stamp_items(d, doffs)
+    torch.cuda.synchronize()
+    assert nbad == 0 and bool(ok.all())
+    stamped = im[:, 28:32].contiguous().cpu().numpy().view(np.uint32).reshape(n)
+    np.testing.assert_array_equal(stamped, want)
+    ok, nbad = mc.verify_items(d, doffs)
+    assert nbad == 0 and bool(ok.all())
+    victims = np.arange(7, n, 1000)
+    im[torch.from_numpy(victims).cuda(), 2000] ^= 0x40
+    ok, nbad = mc.verify_items(d, doffs)
+    assert nbad == victims.size
+    np.testing.assert_array_equal(np.flatnonzero(ok.cpu().numpy() == 0), victims)
+
+
 def _expected_verdicts(buf, offs, wbuf):
     """The oracle's verdict per image, as the library defines it: the header
     parses to a span inside the buffer and inside the image's wbuf, nkey != 0,
