@@ -253,6 +253,10 @@ constexpr uint32_t kWhole = 0xffffffffu;      // unit segment index: the whole s
 constexpr uint32_t kZeroSlots = 256;
 constexpr uint64_t kZeroBytes = 4096ull * kZeroSlots;
 
+// Rows of the shift table (SpanArgs::segpow) below its second-factor rows:
+// units ending less than 16 MiB before their span's end take one multiply.
+constexpr uint32_t kSegpowLo = 4096;
+
 struct SpanArgs {
     const uint8_t *base;       // all spans live in [base, base + base_bytes)
     uint64_t base_bytes;
@@ -275,7 +279,9 @@ struct SpanArgs {
     const struct UnitRec *units;
     const uint32_t *nunits;    // device-side unit count
     uint32_t *span_acc;        // planned batches: R per span (segment units XOR their shifted values in)
-    const uint32_t *segpow;    // rows k (x^i * x^(8 * 64Ki * k), i < 32) for k < 256, then k = 256 j
+    const uint32_t *segpow;    // rows k (x^i * x^(8 * 4096 * k), i < 32) for k < kSegpowLo, then k = kSegpowLo j
+    const uint32_t *starts;    // balanced plan: group g's records are [starts[g], starts[g + 1])
+                               // (0xffffffff: *nunits); nullptr: round robin over units
     uint64_t region;           // MODE 1: items never cross a multiple of `region` (0: no bound)
     uint32_t cfl;              // MODE 1/2: bytes of the ITEM_CFLAGS suffix, sizeof(client_flags_t):
                                // 4, or 8 in a LARGE_CLIENT_FLAGS build (memcached.h:96-100)
@@ -582,7 +588,8 @@ __device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
 
 // Work-unit record written by k_expand (32 B, one dwordx4 pair per unit):
 //   a = {offset of the unit's first byte from base (lo, hi), e - p, E - p}
-//   b = {z (the span's item record), span index, flags | niters << 8, nseg - 1 - segment}
+//   b = {z (the span's item record), span index, flags | niters << 8,
+//        4 KiB blocks from e to the span's end: 16 (nseg - 1 - segment), more for a piece}
 struct alignas(16) UnitRec {
     uint4 a, b;
 };
@@ -628,8 +635,27 @@ __device__ __forceinline__ UnitRec make_unit(const uint8_t *base, uint64_t off, 
     r.b = make_uint4(aux, item,
                      UnitDesc::kValid | (single ? UnitDesc::kSingle : 0u) | (head ? UnitDesc::kHead : 0u) |
                          (sane ? UnitDesc::kSane : 0u) | (niters << 8),
-                     single ? 0u : nseg - 1 - seg);
+                     single ? 0u : (nseg - 1 - seg) * (kSegBytes / kBlockBytes));
     return r;
+}
+
+// Blocks [k0, k1) of unit r (niters nb) as a record of their own: its end
+// moves back by nb - k1 blocks (added to its shift), its start (k0 > 0) to
+// block k0's grid point, which is 16-B aligned (the grid is anchored at the
+// 16-aligned unit end), so the piece's own grid is the unit's.  A piece is
+// never stored whole (not single): its value is shifted and XORed into the
+// span's accumulator.  k0 == k1: an empty record (flags 0).
+__device__ __forceinline__ UnitRec unit_piece(const UnitRec &r, uint32_t k0, uint32_t k1) {
+    const uint32_t nb = r.b.z >> 8;
+    if (k0 == 0 && k1 == nb) return r;
+    UnitRec q{};
+    if (k0 == k1) return q;
+    const uint32_t delta = k0 ? r.a.z - kBlockBytes * (nb - k0) : 0u;  // block k0's G - p
+    const uint64_t o = ((uint64_t)r.a.x | ((uint64_t)r.a.y << 32)) + delta;
+    q.a = make_uint4((uint32_t)o, (uint32_t)(o >> 32), r.a.z - kBlockBytes * (nb - k1) - delta, r.a.w - delta);
+    q.b = make_uint4(r.b.x, r.b.y, (r.b.z & (UnitDesc::kValid | UnitDesc::kSane)) | ((k1 - k0) << 8),
+                     r.b.w + (nb - k1));
+    return q;
 }
 
 // Raw fetch of unit u.  The record is the same for every lane of a group, so
@@ -787,9 +813,14 @@ template <bool UNITS>
 __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *__restrict__ img) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint64_t nunits = UNITS ? (uint64_t)*a.nunits : a.n;
+    // Balanced plan (k_expand): group g takes the records [starts[g],
+    // starts[g + 1]), an equal share of the batch's blocks; else group g takes
+    // units g, g + G, g + 2G, ...
+    const bool bal = UNITS && a.starts;
+    const uint32_t g0 = blockIdx.x * (blockDim.x >> 5);
     // a workgroup without a unit leaves before loading 160 KiB of tables (the
     // overlap pass is usually empty, and small plans do not fill the grid)
-    if ((uint64_t)blockIdx.x * (blockDim.x >> 5) >= nunits) return;
+    if (bal ? (g0 && a.starts[g0] >= nunits) : (uint64_t)g0 >= nunits) return;
     load_tables(smem, img, kLdsImageK1Bytes);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t li = lane & 31u;
@@ -797,16 +828,23 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
     c.lane4 = li << 2;
     c.lane4hi = c.lane4 | 0x10000u;
     const uint64_t ngroups_total = (uint64_t)gridDim.x * (blockDim.x >> 5);
-    uint64_t u = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+    const uint32_t g = g0 + ((threadIdx.x >> 6) << 1) + (lane >> 5);
+    uint64_t u = g;
+    uint64_t ub = nunits;  // the group's records end here
+    if (bal) {
+        u = g ? min(a.starts[g], (uint32_t)nunits) : 0u;
+        ub = min(a.starts[g + 1], (uint32_t)nunits);
+    }
+    const uint64_t ustep = bal ? 1u : ngroups_total;
 
-    UnitDesc cur = decode_unit<UNITS>(a, fetch_unit<UNITS>(a, u, nunits, li), u, nunits, lane);
+    UnitDesc cur = decode_unit<UNITS>(a, fetch_unit<UNITS>(a, u, ub, li), u, nunits, lane);
     // Ring of the next four units' raw records, lane-distributed: lanes
     // 8s..8s+7 of a group hold slot s.  The unit after cur is in slot sl; a
     // switch decodes it and refills the slot with the unit four further on.
     // Nothing is copied out of the ring and no load is used right after it is
     // issued (vmcnt counts in issue order: either would make the wave wait
     // for the block prefetch too).
-    uint32_t ring = fetch_unit<UNITS>(a, u + (1 + (li >> 3)) * ngroups_total, nunits, li);
+    uint32_t ring = fetch_unit<UNITS>(a, u + (1 + (li >> 3)) * ustep, ub, li);
     const uint32_t *const segpow_rows = a.segpow;
     uint32_t sl = 0;
     uint32_t k = 0;    // block index inside cur
@@ -824,9 +862,9 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         if (__any(last)) {
             const uint32_t g = lane & 32u, sb = sl << 3;
             const uint32_t rw = __shfl(ring, g | sb | (li & 7u), 64);  // slot sl, dword li & 7
-            nd = decode_unit<UNITS>(a, rw, u + ngroups_total, nunits, lane);
+            nd = decode_unit<UNITS>(a, rw, u + ustep, nunits, lane);
         }
-        if (last && (li >> 3) == sl) ring = fetch_unit<UNITS>(a, u + 5 * ngroups_total, nunits, li);
+        if (last && (li >> 3) == sl) ring = fetch_unit<UNITS>(a, u + 5 * ustep, ub, li);
         // a segment unit's shift row, loaded after the (masked) ring refill and
         // before the block prefetch: the multiply below then waits for exactly
         // the block's loads issued after it, vmcnt(8), not for everything
@@ -835,7 +873,8 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         uint32_t segk = 0, fx1 = 0;
         if (UNITS) {
             segk = __shfl(cur.raw, (lane & 32u) | 7u, 64);
-            if (__builtin_amdgcn_readfirstlane(__any(last && !cur.single()))) fx1 = segpow_rows[32 * (segk & 255u) + li];
+            if (__builtin_amdgcn_readfirstlane(__any(last && !cur.single())))
+                fx1 = segpow_rows[32 * (segk & (kSegpowLo - 1)) + li];
             __builtin_amdgcn_sched_barrier(0);  // (issued before the block prefetch, not sunk after it)
         }
         {
@@ -884,18 +923,20 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
                     if (cur.single()) {
                         if (li == 0) a.span_acc[item] = raw;
                     } else {
-                        // segment s of nseg: R(span) gets M_{64Ki * (nseg-1-s)}(R)
-                        // (the second factor, for spans past 16 MiB only, is loaded here:
+                        // a segment or piece ending segk blocks before the span's end:
+                        // R(span) gets M_{4096 segk}(R) (the second factor, for units
+                        // 16 MiB or more before the end only, is loaded here:
                         // one register fewer across the step, a drain only at such segment ends)
                         uint32_t v = mul_row_group(raw, fx1, li);
-                        if (__any(segk >= 256u)) v = mul_row_group(v, segpow_rows[32 * (256 + (segk >> 8)) + li], li);
+                        if (__any(segk >= kSegpowLo))
+                            v = mul_row_group(v, segpow_rows[32 * (kSegpowLo + segk / kSegpowLo) + li], li);
                         if (li == 0) atomicXor(a.span_acc + item, v);
                     }
                 }
             }
             acc = 0;
             k = 0;
-            u += ngroups_total;
+            u += ustep;
             cur = nd;
             sl = (sl + 1u) & 3u;
         } else {
@@ -927,20 +968,36 @@ __device__ __forceinline__ uint32_t span_units(const uint8_t *p, uint32_t len) {
     return ns - (h.drop && h.g1o == vlen - (uint64_t)(ns - 1) * kSegBytes ? 1u : 0u);
 }
 
-// Units per span (for the exclusive scan that places the work units), and
+// 4 KiB blocks of those nu units: 16 per segment, and the head segment's
+// niters (make_unit) when it is one of them.
+__device__ __forceinline__ uint32_t span_blocks(const uint8_t *p, uint32_t len, uint32_t nu) {
+    if (nu == 0) return 0;
+    const uint32_t vlen = len + tail_pad(p, len);
+    const uint32_t ns = nseg_of(vlen);
+    constexpr uint32_t kSegBlocks = kSegBytes / kBlockBytes;
+    if (nu < ns) return kSegBlocks * nu;
+    const SpanHead h = span_head(p, len);
+    const uint32_t po = h.drop ? (uint32_t)h.g1o : 0u;
+    const uint32_t eo = vlen - (ns - 1) * kSegBytes - po;
+    return (eo + (uint32_t)((uintptr_t)(p + po) & 15u) + kBlockBytes - 1) / kBlockBytes + kSegBlocks * (ns - 1);
+}
+
+// Units and blocks per span (packed, units | blocks << 32: one exclusive scan
+// places the work units and the balanced plan's group boundaries), and
 // the span's item record with its z (the header is parsed once per launch, and
 // the foreign bytes of the head and tail pieces are read here: for packed
 // images they share lines with the headers this pass reads anyway).
 // Span i's plan entries: one-block flag, unit count, item record, R = 0.
 template <int MODE>
 __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const ItemDesc &it, const Tab8 &t8,
-                                           uint32_t *nunit, uint4 *irec, uint8_t *fast) {
+                                           uint64_t *nunit, uint4 *irec, uint8_t *fast) {
     // a span whose unit is one whole block goes to k_blocks (no units)
     const uint8_t *g1;
     bool none;
     const bool one = it.sane && one_block(it.p, it.len, &g1, &none) && !none;
     fast[i] = one;
-    nunit[i] = one ? 0u : span_units(it.p, it.len);
+    const uint32_t nu = one ? 0u : span_units(it.p, it.len);
+    nunit[i] = nu | (uint64_t)span_blocks(it.p, it.len, nu) << 32;
     const uint64_t off = (uint64_t)(it.p - a.base);
     uint32_t z = 0;
     if (it.sane) {
@@ -952,7 +1009,7 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
 }
 
 template <int MODE>
-__global__ void k_count(SpanArgs a, uint32_t *nunit, uint4 *irec, uint8_t *fast) {
+__global__ void k_count(SpanArgs a, uint64_t *nunit, uint4 *irec, uint8_t *fast) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     __shared__ __attribute__((aligned(16))) uint32_t s8[kTab8Dwords];
     const Tab8 t8 = load_tab8(s8, a.tab8);
@@ -963,8 +1020,8 @@ __global__ void k_count(SpanArgs a, uint32_t *nunit, uint4 *irec, uint8_t *fast)
 
 // Write the unit records of span i at prefix[i].  Spans whose units would pass
 // `cap` (possible only when spans overlap) are listed in `whole` and processed
-// as one unit each by a second pass; *nvalid = units written before the first
-// such span.  Spans of more than kExpandInline segments are listed in `big`
+// as one unit each by a second pass; *nvalid = records written before the
+// first such span (zeroed by the caller: none fit).  Spans of more than kExpandInline segments are listed in `big`
 // and expanded by k_expand_big, one workgroup per span.
 constexpr uint32_t kExpandInline = 32;
 
@@ -973,45 +1030,109 @@ __device__ __forceinline__ uint32_t first_seg(const uint8_t *p, uint32_t len, ui
     return nunit ? nseg_of(len + tail_pad(p, len)) - nunit : 0u;
 }
 
-__global__ void k_expand(const uint8_t *base, const uint32_t *nunit, const uint32_t *prefix, const uint4 *irec,
+// Balanced plan (starts != nullptr).  T = the blocks of all units, G = the
+// span kernel's 32-lane groups: group g's share starts at block g * per,
+// per = ceil(T / G).  A unit holding such boundaries is written as pieces cut
+// at them (unit_piece), so unit j, first block bs, lands at record j + C(bs),
+// C(bs) = the boundaries before bs, and group g's first record is
+// starts[g] = j_g + g (j_g: the unit holding block g * per).  A boundary at a
+// unit's first block leaves an empty record, the end of group g - 1's list.
+// Round robin (starts == nullptr): unit j is record j.
+struct Balance {
+    uint32_t *starts;
+    uint64_t per;  // blocks per group
+    uint64_t gm;   // groups with blocks: boundaries 1 .. gm - 1
+};
+
+__device__ __forceinline__ Balance balance_of(const uint64_t *nunit, const uint64_t *prefix, uint64_t n,
+                                              uint32_t groups, uint32_t *starts) {
+    Balance b{starts, 1, 0};
+    if (starts && n) {
+        const uint64_t t = (prefix[n - 1] + nunit[n - 1]) >> 32;
+        b.per = max((t + groups - 1) / groups, (uint64_t)1);
+        b.gm = (t + b.per - 1) / b.per;
+    }
+    return b;
+}
+
+__device__ __forceinline__ uint64_t cuts_before(const Balance &b, uint64_t bs) {
+    if (!b.starts || bs == 0 || b.gm == 0) return 0;
+    return min((bs + b.per - 1) / b.per - 1, b.gm - 1);
+}
+
+// Write unit j (record r, first block bs) as its records.
+__device__ __forceinline__ void put_unit(UnitRec *units, const Balance &b, uint64_t j, uint64_t bs, const UnitRec &r) {
+    if (!b.starts) {
+        units[j] = r;
+        return;
+    }
+    uint64_t idx = j + cuts_before(b, bs);
+    const uint32_t nb = r.b.z >> 8;
+    uint32_t k0 = 0;
+    for (uint64_t g = max((bs + b.per - 1) / b.per, (uint64_t)1); g < b.gm && g * b.per < bs + nb; ++g) {
+        const uint32_t kb = (uint32_t)(g * b.per - bs);
+        units[idx] = unit_piece(r, k0, kb);
+        b.starts[g] = (uint32_t)(idx + 1);
+        ++idx;
+        k0 = kb;
+    }
+    units[idx] = unit_piece(r, k0, nb);
+}
+
+__global__ void k_expand(const uint8_t *base, const uint64_t *nunit, const uint64_t *prefix, const uint4 *irec,
                          uint64_t n, UnitRec *units, uint64_t cap, uint32_t *nvalid, UnitRec *whole,
-                         uint32_t *nwhole, uint32_t *big, uint32_t *nbig) {
+                         uint32_t *nwhole, uint32_t *big, uint32_t *nbig, uint32_t groups, uint32_t *starts) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
+    const Balance bal = balance_of(nunit, prefix, n, groups, starts);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t p0 = prefix[i], ns = nunit[i];
+        const uint64_t pk = prefix[i], ck = nunit[i];
+        const uint64_t p0 = (uint32_t)pk, ns = (uint32_t)ck, b0 = pk >> 32;
         const uint4 r = irec[i];
         const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
         const bool sane = !(r.y & kInsane);
         if (p0 + ns <= cap) {
             const uint32_t s0 = first_seg(base + off, r.z, (uint32_t)ns);
-            if (ns > kExpandInline)
+            if (ns > kExpandInline) {
                 big[atomicAdd(nbig, 1u)] = (uint32_t)i;
-            else
-                for (uint32_t s = 0; s < ns; ++s)
-                    units[p0 + s] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, s0 + s);
-            if (i + 1 == n) *nvalid = (uint32_t)(p0 + ns);
+            } else {
+                uint64_t bs = b0;
+                for (uint32_t s = 0; s < ns; ++s) {
+                    const UnitRec u = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, s0 + s);
+                    put_unit(units, bal, p0 + s, bs, u);
+                    bs += u.b.z >> 8;
+                }
+            }
+            // the last span whose units fit: the record count
+            if (i + 1 == n || (uint64_t)(uint32_t)prefix[i + 1] + (uint32_t)nunit[i + 1] > cap)
+                *nvalid = (uint32_t)(p0 + ns + cuts_before(bal, b0 + (ck >> 32)));
         } else {
-            if (p0 <= cap) atomicMin(nvalid, (uint32_t)p0);
             // (one unit with the span's head rule: the same grid, so the same G1)
             whole[atomicAdd(nwhole, 1u)] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, kWhole);
         }
     }
 }
 
-__global__ void k_expand_big(const uint8_t *base, const uint32_t *nunit, const uint32_t *prefix, const uint4 *irec,
-                             UnitRec *units, const uint32_t *big, const uint32_t *nbig) {
+__global__ void k_expand_big(const uint8_t *base, const uint64_t *nunit, const uint64_t *prefix, const uint4 *irec,
+                             UnitRec *units, const uint32_t *big, const uint32_t *nbig, uint64_t n, uint32_t groups,
+                             uint32_t *starts) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
+    const Balance bal = balance_of(nunit, prefix, n, groups, starts);
     const uint32_t nb = *nbig;
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint32_t i = big[b];
-        const uint64_t p0 = prefix[i];
-        const uint32_t ns = nunit[i];
+        const uint64_t pk = prefix[i];
+        const uint64_t p0 = (uint32_t)pk, b0 = pk >> 32;
+        const uint32_t ns = (uint32_t)nunit[i];
         const uint4 r = irec[i];
         const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
+        const bool sane = !(r.y & kInsane);
         const uint32_t s0 = first_seg(base + off, r.z, ns);
+        // every unit after the first is a whole segment
+        const uint32_t nb0 = make_unit(base, off, r.z, r.w, sane, i, s0).b.z >> 8;
         for (uint32_t s = threadIdx.x; s < ns; s += blockDim.x)
-            units[p0 + s] = make_unit(base, off, r.z, r.w, !(r.y & kInsane), i, s0 + s);
+            put_unit(units, bal, p0 + s, b0 + (s ? nb0 + (s - 1) * (kSegBytes / kBlockBytes) : 0u),
+                     make_unit(base, off, r.z, r.w, sane, i, s0 + s));
     }
 }
 
@@ -1715,7 +1836,7 @@ struct WalkOut {
     uint32_t *cnt;           // count pass: items per wbuf
     const uint32_t *prefix;  // emit pass: index of each wbuf's first item (nw + 1 entries)
     uint64_t *offs;          // emit pass: item offsets from base
-    uint32_t *nunit;         // emit pass, planned verify (else nullptr): k_count's entries
+    uint64_t *nunit;         // emit pass, planned verify (else nullptr): k_count's entries
     uint4 *irec;
     uint8_t *fast;
     unsigned long long *err; // emit pass: wbufs whose two walks disagree (must stay 0)

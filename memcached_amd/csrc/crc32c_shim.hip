@@ -111,8 +111,10 @@ struct Device {
     uint32_t *hlens[2] = {nullptr, nullptr}, *hcin[2] = {nullptr, nullptr}, *hout[2] = {nullptr, nullptr};
     uint64_t slot_items = 0;
     // work-unit planning for long / variable spans (grow-only)
-    uint32_t *nunit = nullptr, *prefix = nullptr, *span_acc = nullptr, *counters = nullptr;
-    uint32_t *segpow = nullptr;  // rows x^i * x^(8*64Ki*k): k < 256, then k = 256 j
+    uint64_t *nunit = nullptr, *prefix = nullptr;  // per span: units | blocks << 32, and its exclusive scan
+    uint32_t *span_acc = nullptr, *counters = nullptr;
+    uint32_t *starts = nullptr;  // balanced plan: first record of each span-kernel group (groups + 1)
+    uint32_t *segpow = nullptr;  // rows x^i * x^(8*4096*k): k < 256, then k = 256 j
     mcrc_dev::UnitRec *units = nullptr, *whole = nullptr;
     uint4 *irec = nullptr;  // per-span record written by k_count
     uint8_t *fast = nullptr;     // per span: its unit is one whole block (k_blocks takes it)
@@ -230,13 +232,15 @@ int init_device(Device &d, int id) {
     mcrc::build_lds_image_k1(img_k1.data(), mcrc_dev::kK1CH);
     HIP_OK(hipMalloc(&d.img_k1, img_k1.size() * 4));
     HIP_OK(hipMemcpy(d.img_k1, img_k1.data(), img_k1.size() * 4, hipMemcpyHostToDevice));
-    // rows k (k < 256) and 256 + j (x^(8 * kSegBytes * 256 j)) for every
-    // segment count of a 4 GiB span
-    const uint32_t nhi = (uint32_t)((((1ull << 32) + 16) / mcrc_dev::kSegBytes + 1 + 255) / 256);
-    std::vector<uint32_t> sp((256 + std::max(nhi, 256u)) * 32);
-    for (uint32_t k = 0; k < 256 + std::max(nhi, 256u); ++k) {
-        const uint64_t segs = k < 256 ? k : 256ull * (k - 256);
-        const uint32_t y = mcrc::xpow8n((uint64_t)mcrc_dev::kSegBytes * segs);
+    // rows k (k < kSegpowLo) and kSegpowLo + j (x^(8 * 4096 * kSegpowLo j))
+    // for every block shift in a 4 GiB span (a unit's shift: the blocks from
+    // its end to the span's end)
+    constexpr uint32_t lo = mcrc_dev::kSegpowLo;
+    const uint32_t nhi = (uint32_t)((((1ull << 32) + 16) / mcrc_dev::kBlockBytes + 1 + lo - 1) / lo);
+    std::vector<uint32_t> sp((lo + nhi) * 32);
+    for (uint32_t k = 0; k < lo + nhi; ++k) {
+        const uint64_t blocks = k < lo ? k : (uint64_t)lo * (k - lo);
+        const uint32_t y = mcrc::xpow8n((uint64_t)mcrc_dev::kBlockBytes * blocks);
         for (uint32_t i = 0; i < 32; ++i) sp[k * 32 + i] = mcrc::mulmodp(0x80000000u >> i, y);
     }
     HIP_OK(hipMalloc(&d.segpow, sp.size() * 4));
@@ -314,6 +318,16 @@ int grid_for(const Device &d, uint64_t n) {
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
+// Planned batches split their blocks evenly over the span kernel's 32-lane
+// groups (k_expand's balanced plan).  Built with -DMCRC_SPAN_RR: round robin
+// over units (the A/B baseline).
+#ifdef MCRC_SPAN_RR
+constexpr bool kSpanBalance = false;
+#else
+constexpr bool kSpanBalance = true;
+#endif
+uint32_t span_groups(const Device &d) { return (uint32_t)d.cus * (mcrc_dev::kSpanBlock / 32); }
+
 int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
     if (d.plan_items < n) {
         (void)hipFree(d.nunit);
@@ -325,7 +339,7 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
         (void)hipFree(d.fast);
         (void)hipFree(d.fastidx);
         d.plan_items = 0;
-        if (hipMalloc(&d.nunit, n * 4) != hipSuccess || hipMalloc(&d.prefix, n * 4) != hipSuccess ||
+        if (hipMalloc(&d.nunit, n * 8) != hipSuccess || hipMalloc(&d.prefix, n * 8) != hipSuccess ||
             hipMalloc(&d.whole, n * sizeof(mcrc_dev::UnitRec)) != hipSuccess ||
             hipMalloc(&d.irec, n * sizeof(uint4)) != hipSuccess || hipMalloc(&d.span_acc, n * 4) != hipSuccess ||
             hipMalloc(&d.big, n * 4) != hipSuccess || hipMalloc(&d.fast, n) != hipSuccess ||
@@ -347,11 +361,13 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
     if (d.plan_units < cap) {
         (void)hipFree(d.units);
         d.plan_units = 0;
-        if (hipMalloc(&d.units, cap * sizeof(mcrc_dev::UnitRec)) != hipSuccess)
+        // (+ one record per group boundary of the balanced plan)
+        if (hipMalloc(&d.units, (cap + span_groups(d)) * sizeof(mcrc_dev::UnitRec)) != hipSuccess)
             return CRC32C_ENOMEM;
         d.plan_units = cap;
     }
     if (!d.counters && hipMalloc(&d.counters, 16) != hipSuccess) return CRC32C_ENOMEM;
+    if (!d.starts && hipMalloc(&d.starts, (span_groups(d) + 1) * 4) != hipSuccess) return CRC32C_ENOMEM;
     return CRC32C_OK;
 }
 
@@ -496,8 +512,8 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     int rc = ensure_plan(d, n, cap);
     if (rc) return rc;
     uint32_t *nvalid = d.counters, *nwhole = d.counters + 1, *nbig = d.counters + 2, *nfast = d.counters + 3;
-    HIP_OK(hipMemsetAsync(nvalid, 0xff, 4, st));
-    HIP_OK(hipMemsetAsync(nwhole, 0, 8, st));  // nwhole, nbig
+    HIP_OK(hipMemsetAsync(nvalid, 0, 12, st));  // nvalid, nwhole, nbig
+    if (kSpanBalance) HIP_OK(hipMemsetAsync(d.starts, 0xff, (span_groups(d) + 1) * 4, st));
     a.span_acc = d.span_acc;
     if (!path.counted)
         hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nunit, d.irec, d.fast);
@@ -506,15 +522,17 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     tmp = d.scan_tmp_bytes;
     HIP_OK(hipcub::DeviceSelect::Flagged(d.scan_tmp, tmp, hipcub::CountingInputIterator<uint32_t>(0), d.fast,
                                          d.fastidx, nfast, (int)n, st));
+    uint32_t *const starts = kSpanBalance ? d.starts : nullptr;
     hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(g1), dim3(256), 0, st, a.base, d.nunit, d.prefix, d.irec, n, d.units,
-                       cap, nvalid, d.whole, nwhole, d.big, nbig);
+                       cap, nvalid, d.whole, nwhole, d.big, nbig, span_groups(d), starts);
     hipLaunchKernelGGL(mcrc_dev::k_expand_big, dim3(1024), dim3(256), 0, st, a.base, d.nunit, d.prefix, d.irec,
-                       d.units, d.big, nbig);
+                       d.units, d.big, nbig, n, span_groups(d), starts);
     mcrc_dev::SpanArgs u = a;
     u.units = d.units;
     u.nunits = nvalid;
     u.span_acc = d.span_acc;
     u.segpow = d.segpow;
+    u.starts = starts;
     // spans whose unit is one whole block: k_blocks over the compacted list;
     // the other spans' units: the span kernel
     hipLaunchKernelGGL((mcrc_dev::k_blocks<false, true>), dim3(grid_for(d, n)), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st,
@@ -523,6 +541,7 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     mcrc_dev::SpanArgs w = u;  // (every table pointer set, even those whole units do not use)
     w.units = d.whole;
     w.nunits = nwhole;
+    w.starts = nullptr;
     spans(w, d.cus);
     hipLaunchKernelGGL((mcrc_dev::k_final<MODE, true>), dim3(gf), dim3(256), 0, st, u, d.irec);
     HIP_OK(hipGetLastError());

@@ -147,3 +147,68 @@ def one_block(p, length):
     if not drop and x == BLOCK:  # the unit [ph, Ea) is itself one block
         return True, False, p - kh
     return none or (drop and vlen - g1o == BLOCK), none, p + g1o
+
+
+# --- balanced plan (crc32c_kernels.hip span_blocks, unit_piece, put_unit) ---
+
+SEG_BLOCKS = SEG // BLOCK
+
+
+def span_blocks(p, length):
+    """4 KiB blocks of the span's work units (span_blocks)."""
+    nu = span_units(p, length)
+    if nu == 0:
+        return 0
+    vlen = length + tail_pad(p, length)
+    ns = nseg_of(vlen)
+    if nu < ns:
+        return SEG_BLOCKS * nu
+    g1o, drop = span_head(p, length)
+    po = g1o if drop else 0
+    eo = vlen - (ns - 1) * SEG - po
+    return (eo + ((p + po) & 15) + BLOCK - 1) // BLOCK + SEG_BLOCKS * (ns - 1)
+
+
+def unit_piece(unit, k0, k1):
+    """Blocks [k0, k1) of unit (p, eo, niters, single, shift in blocks) as a
+    record of their own; None for an empty one (unit_piece)."""
+    p, eo, nb, single, shift = unit
+    if k0 == 0 and k1 == nb:
+        return unit
+    if k0 == k1:
+        return None
+    delta = eo - BLOCK * (nb - k0) if k0 else 0
+    return (p + delta, eo - BLOCK * (nb - k1) - delta, k1 - k0, False, shift + nb - k1)
+
+
+def balanced_plan(spans, groups):
+    """Records and group starts of a batch [(p, length), ...] for `groups`
+    32-lane groups (k_expand + k_expand_big with a balanced plan).  Returns
+    (records, starts, per): records[i] = (span, record) with record as in
+    unit_piece, starts[g] = group g's first record (g = 1 .. groups - 1 with
+    blocks; groups past the last have none)."""
+    units = []  # (span, unit with its shift in blocks)
+    for s, (p, length) in enumerate(spans):
+        for up, eo, nb, single, segk in units_of(0, p, length):
+            units.append((s, (up, eo, nb, single, SEG_BLOCKS * segk)))
+    t = sum(u[2] for _, u in units)
+    per = max(-(-t // groups), 1)
+    gm = -(-t // per)
+    starts = {0: 0}
+    records = []
+    bs = 0
+    for j, (s, u) in enumerate(units):
+        nb = u[2]
+        cuts = min(-(-bs // per) - 1, gm - 1) if bs and gm else 0
+        assert len(records) == j + cuts  # the record index k_expand computes
+        k0 = 0
+        g = max(-(-bs // per), 1)
+        while g < gm and g * per < bs + nb:
+            kb = g * per - bs
+            records.append((s, unit_piece(u, k0, kb)))
+            starts[g] = len(records)
+            k0 = kb
+            g += 1
+        records.append((s, unit_piece(u, k0, nb)))
+        bs += nb
+    return records, starts, per
