@@ -113,13 +113,13 @@ def splitmix64_bytes(nbytes: int, seed: int, chunk_words: int = 1 << 26, device:
     return words.view(torch.uint8)
 
 
-def make_batch(n: int, seed: int, fill: str = "splitmix"):
+def make_batch(n: int, seed: int, fill: str = "splitmix", device: str = "cuda"):
     if fill == "splitmix":
-        data = splitmix64_bytes(n * ITEM_BYTES, seed)
+        data = splitmix64_bytes(n * ITEM_BYTES, seed, device=device)
     else:
-        g = torch.Generator(device="cuda").manual_seed(seed)
-        data = torch.randint(0, 256, (n * ITEM_BYTES,), dtype=torch.uint8, device="cuda", generator=g)
-    out = torch.empty(n, dtype=torch.int32, device="cuda")
+        g = torch.Generator(device=device).manual_seed(seed)
+        data = torch.randint(0, 256, (n * ITEM_BYTES,), dtype=torch.uint8, device=device, generator=g)
+    out = torch.empty(n, dtype=torch.int32, device=device)
     spans = _lib.Spans(data.data_ptr(), data.numel(), None, ITEM_BYTES, None, ITEM_BYTES, None,
                        out.data_ptr(), n)
     return data, out, spans
@@ -432,7 +432,7 @@ def traffic_per_launch(items=ITEMS_PER_GPU, item_bytes=ITEM_BYTES):
     return None
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # defaults: 50 timed launches after 20 untimed ones -- the core clock takes
@@ -454,9 +454,12 @@ def main():
                     help="config2 = headline; others are extra measurements (not the bench line)")
     ap.add_argument("--pages", type=int, default=1000, help="config5: 64 MiB pages per GPU")
     ap.add_argument("--span-len", type=int, default=4133, help="config2r: span length (stride = len + 32)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.workload != "config2":
         return extra_workload(args)
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        # no launcher: one process drives the N devices itself
+        return headline_devices(args)
 
     rank, world, local = dist_setup(args.gpus)
     if _lib.lib.crc32c_gpu_count() < 1:
@@ -477,16 +480,28 @@ def main():
 
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     kernel_ms = max_over_ranks(kernel_ms, world)
-    bytes_per_launch = n * ITEM_BYTES
-    total_bytes = bytes_per_launch * args.steps * world
-    value = total_bytes / elapsed / 2**30
-    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    value = n * ITEM_BYTES * args.steps * world / elapsed / 2**30
 
-    result = {
+    result = headline_result(args, value, elapsed, kernel_ms, world, settled,
+                             f"items sharded across {world} rank(s), no collective on the data path")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU leg runs at N = 1 only
+        result["cpu_baseline"] = cpu_baseline(data, out)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def headline_result(args, value, elapsed, kernel_ms, n_gpus, settled, parallelism):
+    """The bench line's fields (kernel_ms: the slowest device's average K1
+    launch, HIP events on its launch stream)."""
+    achieved = args.items * ITEM_BYTES / (kernel_ms * 1e-3) / 1e9
+    return {
         "metric": "CRC32C GiB/s over device-resident item batches; % of HBM roofline",
         "value": round(value, 2),
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "settle": {"ms": args.settle_ms, "launches": settled},
@@ -499,9 +514,9 @@ def main():
         "config": {
             "workload": "BASELINE configs[1]: 1 Mi items x 4096 B per GPU, stride 4096, one 32-lane group per "
                         "item (K1 k_fixed<slice-by-4, 32 lanes, 32 B/lane/row, 4 rows, row folds in the last-step tables, four items reduced per tree>)",
-            "items_per_gpu": n,
+            "items_per_gpu": args.items,
             "item_bytes": ITEM_BYTES,
-            "parallelism": f"items sharded across {world} rank(s), no collective on the data path",
+            "parallelism": parallelism,
         },
         "roofline": {
             "bound": "hbm",
@@ -513,13 +528,59 @@ def main():
             "kernel_ms": round(kernel_ms, 4),
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU leg runs at N = 1 only
-        result["cpu_baseline"] = cpu_baseline(data, out)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+
+
+def headline_devices(args):
+    """The headline on --gpus N devices from ONE process (bench.py started
+    without a launcher, WORLD_SIZE unset): device g holds its own 1 Mi x 4 KiB
+    shard (seed 42 + g, as rank g would) and K1 runs on every device, each on
+    its own stream, the K launches of all devices enqueued before any is
+    waited for.  The timed region is bracketed by a synchronize of every
+    device; value = all devices' bytes / that wall time, kernel_ms = the
+    slowest device's average launch.  No data-path collective, as with ranks."""
+    ng = args.gpus
+    vis = torch.cuda.device_count()  # (does not initialise the GPU)
+    if vis < ng:
+        raise SystemExit(f"bench.py: --gpus {ng} but only {vis} visible device(s); run with --gpus <= {vis}")
+    if _lib.lib.crc32c_gpu_count() < ng:
+        raise SystemExit(f"bench.py: --gpus {ng} but libmcrc32c.so sees {_lib.lib.crc32c_gpu_count()} gfx950 device(s)")
+    devs = []
+    for g in range(ng):
+        torch.cuda.set_device(g)
+        data, out, spans = make_batch(args.items, seed=42 + g, fill=args.fill, device=f"cuda:{g}")
+        devs.append((g, data, out, spans, torch.cuda.Stream(device=g)))
+
+    def launch(k, evs=None):
+        flags = _lib.CRC32C_DEVICE | _lib.CRC32C_ASYNC
+        for i in range(k):
+            for g, data, out, sp, st in devs:
+                torch.cuda.set_device(g)  # the library launches on the current device
+                if evs is not None and i == 0:
+                    evs[g][0].record(st)
+                _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp), flags, ctypes.c_void_p(st.cuda_stream)))
+                if evs is not None and i == k - 1:
+                    evs[g][1].record(st)
+
+    def sync_all():
+        for g, *_ in devs:
+            torch.cuda.synchronize(g)
+
+    settled = settle(lambda k: (launch(k), sync_all()), args.settle_ms)
+    launch(max(1, args.warmup))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(ng)]
+    sync_all()
+    t0 = time.perf_counter()
+    launch(args.steps, evs)
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    kms = [evs[g][0].elapsed_time(evs[g][1]) / args.steps for g in range(ng)]
+    value = ng * args.items * ITEM_BYTES * args.steps / elapsed / 2**30
+    result = headline_result(args, value, elapsed, max(kms), ng, settled,
+                             f"items sharded across {ng} devices driven by one process (no launcher), one stream "
+                             "each, no collective on the data path")
+    result["kernel_ms_per_device"] = [round(x, 4) for x in kms]
+    print(json.dumps(result), flush=True)
+    return result
 
 
 def workload_multi(args):

@@ -35,8 +35,13 @@ void crc32c_init(void);
 
 uint32_t crc32c_sw(uint32_t crc, void const *buf, size_t len);
 
-/* Non-static in the reference (crc32c.c:52); exported for completeness. */
+/* Non-static in the reference (crc32c.c:52-53); exported for completeness.
+ * crc32c_sw_big is the big-endian slice-by-8 (crc32c.c:467-498) evaluated
+ * with this host's native loads, exactly as the reference's own symbol: the
+ * CRC-32C on a big-endian host, the reference's same non-CRC function on a
+ * little-endian one (crc32c_sw picks crc32c_sw_little there). */
 uint32_t crc32c_sw_little(uint32_t crc, void const *buf, size_t len);
+uint32_t crc32c_sw_big(uint32_t crc, void const *buf, size_t len);
 
 #ifdef __cplusplus
 }

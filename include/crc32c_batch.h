@@ -59,8 +59,9 @@ extern "C" {
 #define CRC32C_DEVICE 0x1u    /* every pointer in the batch is device memory of the
                                  current HIP device */
 #define CRC32C_ASYNC 0x2u     /* with CRC32C_DEVICE: enqueue on `stream`, do not wait */
-#define CRC32C_ALIGNED16 0x4u /* caller guarantees every span start and length is a
-                                 multiple of 16 bytes (selects the aligned kernel) */
+/* (0x4u is reserved: earlier builds named it CRC32C_ALIGNED16, an alignment
+   promise no kernel needs -- every span kernel reads the 16-B pieces a span
+   overlaps as they lie, at any alignment -- and it is ignored.) */
 #define CRC32C_CFLAGS64 0x8u  /* item-image calls: the images come from a build with
                                  --enable-large-client-flags (configure.ac:139-140):
                                  client_flags_t is 8 bytes, so ITEM_CFLAGS adds 8 to

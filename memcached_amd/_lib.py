@@ -24,13 +24,12 @@ CRC32C_EWALK = -6
 
 CRC32C_DEVICE = 0x1
 CRC32C_ASYNC = 0x2
-CRC32C_ALIGNED16 = 0x4
 CRC32C_CFLAGS64 = 0x8
 CRC32C_MAX_SPAN = 0x7FFF0000  # longest span (include/crc32c_batch.h)
 
 # every symbol include/*.h declares (checked by tests/test_abi.py)
 EXPORTED = (
-    "crc32c", "crc32c_init", "crc32c_sw", "crc32c_sw_little",
+    "crc32c", "crc32c_init", "crc32c_sw", "crc32c_sw_little", "crc32c_sw_big",
     "crc32c_gpu_count", "crc32c_batch", "crc32c_batch_multi", "crc32c_verify_items", "crc32c_stamp_items",
     "crc32c_verify_pages", "crc32c_batch_chains", "crc32c_host_alloc", "crc32c_host_free",
     "crc32c_batch_submit", "crc32c_batch_wait", "crc32c_strerror", "crc32c_last_kernel_ms",

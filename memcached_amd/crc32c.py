@@ -22,7 +22,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import CRC32C_ALIGNED16, CRC32C_ASYNC, CRC32C_CFLAGS64, CRC32C_DEVICE, Crc32cError, check, lib
+from ._lib import CRC32C_ASYNC, CRC32C_CFLAGS64, CRC32C_DEVICE, Crc32cError, check, lib
 
 __all__ = ["crc32c", "crc32c_sw", "batch", "verify_items", "stamp_items", "verify_pages", "batch_chains", "batch_multi",
            "shard_cuts", "queue_stats", "set_small_max", "gpu_count", "Crc32cError"]
@@ -77,7 +77,7 @@ def _check_dev(t, name, n, dtypes):
 
 
 def batch(buf, offsets=None, stride: int = 0, lens=None, length: int = 0, crc_in=None, out=None,
-          aligned16: bool = False, stream=None, asynchronous: bool = False):
+          stream=None, asynchronous: bool = False):
     """Batched CRC-32C of spans of ``buf``.
 
     Span i = buf[off_i : off_i + len_i] with off_i = offsets[i] (or i*stride)
@@ -122,7 +122,7 @@ def batch(buf, offsets=None, stride: int = 0, lens=None, length: int = 0, crc_in
             raise TypeError("out: need a contiguous uint32 array")
     s = _lib.Spans(_ptr(buf), base_bytes, _ptr(offsets), stride, _ptr(lens), length, _ptr(crc_in),
                    _ptr(out), n)
-    flags = (CRC32C_DEVICE if dev else 0) | (CRC32C_ALIGNED16 if aligned16 else 0)
+    flags = CRC32C_DEVICE if dev else 0
     if dev and asynchronous:
         flags |= CRC32C_ASYNC
     check(lib.crc32c_batch(ctypes.byref(s), flags, stream if dev else None), "crc32c_batch")

@@ -90,12 +90,38 @@ __device__ __forceinline__ uint32_t step4_next(uint32_t x, uint32_t w_next, cons
 constexpr uint32_t kAuxShift0 = 156, kAuxShift1 = 24, kAuxShift2 = 20;
 constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 
+#ifndef MCRC_NIB
+#define MCRC_NIB 0
+#endif
+// Nibble form of the shifted tables (MCRC_NIB): set s (row chain s, shift
+// M_{(3-s)*1024}) holds 8 tables of 16 entries, table 2k + h for nibble h of
+// byte k, at kNibShiftBytes + 512 s + 64 (2k + h).  A 16-entry table spans 16
+// banks with one entry per bank, so any 32 lanes read it conflict-free (the
+// byte tables, 8 entries per bank, cost ~2.2 extra LDS cycles per 32 lanes).
+constexpr uint32_t kNibShiftBytes = 20 * 1024;
+constexpr uint32_t nib_set(uint32_t t0) { return t0 == kAuxShift0 ? 0u : t0 == kAuxShift1 ? 1u : 2u; }
+
 // Last slice-by-4 step of a row chain through the shifted tables t0..t0+3:
 // returns M_shift(T3[x0] ^ T2[x1] ^ T1[x2] ^ T0[x3]).
 __device__ __forceinline__ uint32_t step4_last_shifted(uint32_t x, uint32_t t0) {
+#if MCRC_NIB
+    // rotl 2 puts the low nibble of byte k at bits 2..5 of byte k, rotr 2 the
+    // high nibble: each address is one byte of a rotation masked to 0x3c
+    uint32_t lo = __builtin_amdgcn_alignbit(x, x, 30), hi = __builtin_amdgcn_alignbit(x, x, 2);
+    // (opaque to the optimizer: it would fold the rotations into two shifts
+    // per nibble; kept, each address is one SDWA byte-select AND)
+    asm volatile("" : "+v"(lo), "+v"(hi));
+    const uint32_t b = kNibShiftBytes + 512u * nib_set(t0);
+    return xor3(xor3(lds_ld(b + (lo & 0x3cu)), lds_ld(b + 64 + (hi & 0x3cu)), lds_ld(b + 128 + ((lo >> 8) & 0x3cu))),
+                xor3(lds_ld(b + 192 + ((hi >> 8) & 0x3cu)), lds_ld(b + 256 + ((lo >> 16) & 0x3cu)),
+                     lds_ld(b + 320 + ((hi >> 16) & 0x3cu))),
+                lds_ld(b + 384 + ((lo >> 24) & 0x3cu))) ^
+           lds_ld(b + 448 + ((hi >> 24) & 0x3cu));
+#else
     return xor3(Step<4>::aux(t0, x & 0xffu), Step<4>::aux(t0 + 1, (x >> 8) & 0xffu),
                 Step<4>::aux(t0 + 2, (x >> 16) & 0xffu)) ^
            Step<4>::aux(t0 + 3, x >> 24);
+#endif
 }
 
 // Apply the zeros operator stored in aux tables t0..t0+3.

@@ -20,6 +20,7 @@ constexpr size_t kStreamBlock = 4096;  // bytes per stream per round of the 3-wa
 uint32_t g_shift_block[4][256];     // M_{kStreamBlock}
 uint32_t g_shift_small[4][256];     // M_{kSmallBlock}
 constexpr size_t kSmallBlock = 256;
+uint64_t g_big[8][256];             // big-endian word tables: g_slice[k][b] byte-reversed into bits 32..63
 
 void build_all() {
     build_t0(g_slice[0]);
@@ -28,6 +29,8 @@ void build_all() {
             const uint32_t prev = g_slice[k - 1][b];
             g_slice[k][b] = g_slice[0][prev & 0xffu] ^ (prev >> 8);
         }
+    for (int k = 0; k < 8; ++k)
+        for (int b = 0; b < 256; ++b) g_big[k][b] = (uint64_t)__builtin_bswap32(g_slice[k][b]) << 32;
     Gf2Op::zeros(kStreamBlock).byte_tables(g_shift_block);
     Gf2Op::zeros(kSmallBlock).byte_tables(g_shift_small);
 }
@@ -53,6 +56,33 @@ uint32_t reg_sw(uint32_t r, const unsigned char *p, size_t n) {
         r = g_slice[7][x & 0xffu] ^ g_slice[6][(x >> 8) & 0xffu] ^ g_slice[5][(x >> 16) & 0xffu] ^
             g_slice[4][(x >> 24) & 0xffu] ^ g_slice[3][(x >> 32) & 0xffu] ^
             g_slice[2][(x >> 40) & 0xffu] ^ g_slice[1][(x >> 48) & 0xffu] ^ g_slice[0][x >> 56];
+    }
+    while (n--) r = g_slice[0][(r ^ *p++) & 0xffu] ^ (r >> 8);
+    return r;
+}
+
+// The big-endian slice-by-8 of crc32c.c:467-498 (crc32c_sw_big), evaluated
+// with this host's native 64-bit loads, as the reference's exported function
+// is: the register is kept byte-reversed in the upper half of a 64-bit word,
+// each aligned data word (native load) is XORed in, and byte j of the word
+// (j = 0 the low-order byte) indexes the word table of j trailing zero bytes.
+// On a big-endian host that is CRC-32C; on a little-endian host it is the
+// reference's same (non-CRC) function, which callers only reach through
+// crc32c_sw_big itself (crc32c_sw dispatches by endianness, crc32c.c:507-513).
+uint32_t reg_sw_big(uint32_t r, const unsigned char *p, size_t n) {
+    while (n && ((uintptr_t)p & 7u)) {
+        r = g_slice[0][(r ^ *p++) & 0xffu] ^ (r >> 8);
+        --n;
+    }
+    if (n >= 8) {
+        uint64_t w = (uint64_t)__builtin_bswap32(r) << 32;
+        for (; n >= 8; n -= 8, p += 8) {
+            w ^= load64(p);
+            uint64_t acc = 0;
+            for (int j = 0; j < 8; ++j) acc ^= g_big[j][(w >> (8 * j)) & 0xffu];
+            w = acc;
+        }
+        r = (uint32_t)__builtin_bswap64(w);
     }
     while (n--) r = g_slice[0][(r ^ *p++) & 0xffu] ^ (r >> 8);
     return r;
@@ -109,6 +139,11 @@ bool host_has_sse42() {
 uint32_t crc32c_host_sw(uint32_t crc, const void *buf, size_t len) {
     host_tables_init();
     return ~reg_sw(~crc, static_cast<const unsigned char *>(buf), len);
+}
+
+uint32_t crc32c_host_sw_big(uint32_t crc, const void *buf, size_t len) {
+    host_tables_init();
+    return ~reg_sw_big(~crc, static_cast<const unsigned char *>(buf), len);
 }
 
 uint32_t crc32c_host_hw(uint32_t crc, const void *buf, size_t len) {

@@ -16,6 +16,8 @@ namespace mcrc {
 void host_tables_init();  // idempotent, thread-safe
 uint32_t crc32c_host_sw(uint32_t crc, const void *buf, size_t len);
 uint32_t crc32c_host_hw(uint32_t crc, const void *buf, size_t len);
+// crc32c_sw_big (crc32c.c:467-498) as the reference computes it on this host
+uint32_t crc32c_host_sw_big(uint32_t crc, const void *buf, size_t len);
 bool host_has_sse42();
 // crc32c(crc, A || B) from crc32c(crc, A), crc32c(0, B) and |B|.
 uint32_t crc32c_host_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);

@@ -50,6 +50,10 @@ uint32_t crc32c_sw_little(uint32_t crc, void const *buf, size_t len) {
     return mcrc::crc32c_host_sw(crc, buf, len);
 }
 
+uint32_t crc32c_sw_big(uint32_t crc, void const *buf, size_t len) {
+    return mcrc::crc32c_host_sw_big(crc, buf, len);
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

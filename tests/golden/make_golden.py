@@ -15,6 +15,9 @@ Outputs (committed):
   items.npz    memcached item images packed into wbufs (layout.py) with the
                spill CRC (storage.c:567) of every item: config-1 shaped items
                (key%07d, 4096-byte values, CAS) and items of varied geometry
+  swbig.npz    the reference crc32c_sw_big (crc32c.c:467-498) on this host,
+               lengths 0..300 and five long ones at every 8-byte alignment
+               (python tests/golden/make_golden.py --swbig)
   config1.json BASELINE configs[0] in full (python tests/golden/make_golden.py
                --config1): the 10 000 items tests/integration/extstore_config1.c
                spills (value bytes: one splitmix64 stream, seed 1, 8 bytes per
@@ -145,9 +148,40 @@ def config1() -> None:
     print("wrote config1.json", rec["digest"])
 
 
+def sw_big() -> None:
+    """crc32c_sw_big (crc32c.c:467-498), the reference's exported big-endian
+    table routine, on this (little-endian) host: every length 0..300 and a few
+    long ones at every 8-byte alignment of one random buffer, with and without
+    an initial CRC.  (Not CRC-32C on a little-endian host; it pins the
+    library's crc32c_sw_big to the reference symbol's own answers.)"""
+    f = lib.crc32c_sw_big  # the reference's own symbol in oracle/_ref
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+    rng = np.random.default_rng(20261017)
+    buf = rng.integers(0, 256, 4104, dtype=np.uint8)
+    lens = np.concatenate([np.arange(301), [511, 1024, 1031, 4095, 4096]]).astype(np.uint32)
+    cin = rng.integers(0, 2**32, (lens.size, 8), dtype=np.uint64).astype(np.uint32)
+    crc0 = np.zeros((lens.size, 8), np.uint32)
+    crcin = np.zeros((lens.size, 8), np.uint32)
+    # the word loop starts at the first 8-B aligned address, so the answer
+    # depends on the address: spans start at off from an 8-B aligned base
+    cbuf = ctypes.create_string_buffer(buf.tobytes(), buf.size)
+    base = ctypes.addressof(cbuf)
+    assert base % 8 == 0
+    for i, n in enumerate(lens):
+        for off in range(8):
+            crc0[i, off] = f(0, base + off, int(n))
+            crcin[i, off] = f(int(cin[i, off]), base + off, int(n))
+    np.savez_compressed(os.path.join(HERE, "swbig.npz"), buf=buf, lens=lens, cin=cin, crc0=crc0, crcin=crcin)
+    print("wrote swbig.npz")
+
+
 if __name__ == "__main__":
     if "--config1" in sys.argv:
         config1()
+    elif "--swbig" in sys.argv:
+        sw_big()
     else:
         main()
         config1()
+        sw_big()

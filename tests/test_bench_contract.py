@@ -60,3 +60,31 @@ def test_cpu_baseline_runs_the_reference_on_every_core(monkeypatch):
     assert r["kind"] == "reference" and r["cores"] == len(cpus) and r["sockets"] == sockets
     assert r["gpu_match"] is True and r["value"] > 0 and r["one_core"] > 0 and r["cpu_model"] == model
     assert r["value"] == max(r["numa_local"], r["resident"])
+
+
+def test_gpus_n_without_launcher_runs_in_one_process(monkeypatch):
+    """`python bench.py --gpus N` (the driver's form, no torchrun) takes the
+    single-process path over N devices instead of stopping in dist_setup; with
+    fewer visible devices than N it exits with a message naming both counts."""
+    import torch
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    called = {}
+    monkeypatch.setattr(bench, "headline_devices", lambda a: called.setdefault("n", a.gpus))
+    bench.main(["--gpus", "4", "--steps", "3"])
+    assert called == {"n": 4}
+    monkeypatch.undo()
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "2"])
+    assert "--gpus 2" in str(e.value) and "1 visible" in str(e.value)
+
+
+def test_gpus_n_under_a_launcher_keeps_the_rank_path(monkeypatch):
+    """Under torchrun (WORLD_SIZE = N) the rank path runs; a WORLD_SIZE that
+    differs from --gpus is still an error."""
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(bench, "headline_devices", lambda a: pytest.fail("single-process path taken under a launcher"))
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "4"])
+    assert "WORLD_SIZE=2" in str(e.value)

@@ -120,7 +120,9 @@ def test_golden_host_path():
     np.testing.assert_array_equal(out, g["crcin"].reshape(-1)[order])
 
 
-def test_aligned_spans_kernel(torch):
+def test_16b_aligned_spans(torch):
+    """Spans whose starts and lengths are multiples of 16 (no head or tail
+    fragment: the span kernel's pieces are exactly the span)."""
     rng = np.random.default_rng(5)
     n = 3000
     lens = (rng.integers(0, 700, n) * 16).astype(np.uint32)
@@ -128,8 +130,7 @@ def test_aligned_spans_kernel(torch):
     host = rng.integers(0, 256, int(offs[-1] + lens[-1] + 64), dtype=np.uint8)
     want = oracle.batch(host, offs, lens)
     d = _dev(torch, host)
-    out = mc.batch(d, offsets=_dev(torch, offs.view(np.int64)), lens=_dev(torch, lens.view(np.int32)),
-                   aligned16=True)
+    out = mc.batch(d, offsets=_dev(torch, offs.view(np.int64)), lens=_dev(torch, lens.view(np.int32)))
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_u32(out), want)
 
@@ -158,7 +159,8 @@ def test_variable_unaligned_up_to_1mib(torch):
 
 @pytest.mark.parametrize("aligned", [False, True])
 def test_long_spans_cross_segments(torch, aligned):
-    """Spans of several 64 KiB work units: segment split + combine pass."""
+    """Spans of several 64 KiB work units: segment split + combine pass
+    (aligned: every start and length a multiple of 16, the same kernels)."""
     rng = np.random.default_rng(31 + aligned)
     lens = rng.integers(0, 5 << 20, 60).astype(np.uint32)
     lens[:6] = [65536, 65537, 65535, 131072, 131073, (3 << 20) + 5]
@@ -171,7 +173,7 @@ def test_long_spans_cross_segments(torch, aligned):
     want = oracle.batch(host, offs, lens, cin)
     d = _dev(torch, host)
     out = mc.batch(d, offsets=_dev(torch, offs.view(np.int64)), lens=_dev(torch, lens.view(np.int32)),
-                   crc_in=_dev(torch, cin.view(np.int32)), aligned16=aligned)
+                   crc_in=_dev(torch, cin.view(np.int32)))
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_u32(out), want)
 
