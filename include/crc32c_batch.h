@@ -175,8 +175,11 @@ int crc32c_stamp_items(void *base, uint64_t base_bytes, uint64_t region_bytes,
  * IO threads that each submit their few reads (storage.c:172 per io_depth
  * batch) thus share launches; crc32c_batch itself takes this path for such
  * batches.  Other jobs (pageable host memory, long spans, CRC32C_DEVICE
- * batches, which must be complete in device memory when submitted) run one
- * by one on the dispatcher.  The caller's arrays must stay valid until
+ * batches) run one by one on the dispatcher.  A CRC32C_DEVICE job runs on the
+ * queue's own stream after the work the submitting thread had enqueued on its
+ * device's default (NULL) stream when it submitted (an event recorded there
+ * at submit time): a batch filled by work on another stream must be complete
+ * when submitted.  The caller's arrays must stay valid until
  * crc32c_batch_wait returns. */
 typedef struct crc32c_job *crc32c_job_t;
 int crc32c_batch_submit(const crc32c_spans *spans, unsigned flags, crc32c_job_t *job);

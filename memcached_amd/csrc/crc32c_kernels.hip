@@ -1018,7 +1018,123 @@ __global__ void k_count(SpanArgs a, uint64_t *nunit, uint4 *irec, uint8_t *fast)
         count_item<MODE>(a, i, fetch_item<MODE>(a, i), t8, nunit, irec, fast);
 }
 
-// Write the unit records of span i at prefix[i].  Spans whose units would pass
+// ---------------------------------------------------------------------------
+// The plan's prefix sums (round 4: the library's own kernels instead of
+// hipcub's scan and select, so that every kernel that runs several
+// workgroups per CU carries the VGPR floor, crc32c_device.h).  Per span k_count
+// (or the walk) leaves nunit[i] = units | blocks << 32 and fast[i]; tiles of
+// kPlanTile spans are reduced (k_plan_tiles), the tile sums scanned by one
+// workgroup (k_plan_scan), and k_expand rescans its tile to place every span:
+// units and blocks are summed in 64 bits each (no carry between the fields),
+// the fast spans' positions give the compacted list k_blocks reads.
+// ---------------------------------------------------------------------------
+struct PlanSum {
+    uint64_t units, blocks;
+    uint32_t fast, pad;
+};
+constexpr uint32_t kPlanThreads = 256, kPlanPer = 8, kPlanTile = kPlanThreads * kPlanPer;
+
+__device__ __forceinline__ PlanSum plan_of(uint64_t nu, uint8_t f) {
+    return {(uint32_t)nu, nu >> 32, (uint32_t)f, 0u};
+}
+__device__ __forceinline__ PlanSum plan_add(const PlanSum &x, const PlanSum &y) {
+    return {x.units + y.units, x.blocks + y.blocks, x.fast + y.fast, 0u};
+}
+
+// Exclusive scan of v over a 256-thread workgroup; *total = the sum of all.
+// Every thread calls it (two barriers; `sh` holds 4 wave sums).
+__device__ __forceinline__ PlanSum block_scan_excl(PlanSum v, PlanSum *sh, PlanSum *total) {
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    PlanSum inc = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t u = __shfl_up(inc.units, d, 64), b = __shfl_up(inc.blocks, d, 64);
+        const uint32_t f = __shfl_up(inc.fast, d, 64);
+        if (lane >= d) inc = plan_add(inc, PlanSum{u, b, f, 0u});
+    }
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    PlanSum before{0, 0, 0, 0}, all{0, 0, 0, 0};
+    for (uint32_t k = 0; k < kPlanThreads / 64; ++k) {
+        if (k < w) before = plan_add(before, sh[k]);
+        all = plan_add(all, sh[k]);
+    }
+    __syncthreads();  // (sh is reused by the next call)
+    *total = all;
+    return plan_add(before, PlanSum{inc.units - v.units, inc.blocks - v.blocks, inc.fast - v.fast, 0u});
+}
+
+// Span i's count record (past n: zero).
+__device__ __forceinline__ PlanSum plan_at(const uint64_t *nunit, const uint8_t *fast, uint64_t n, uint64_t i) {
+    return i < n ? plan_of(nunit[i], fast[i]) : PlanSum{0, 0, 0, 0};
+}
+
+// Tile t's sum (thread-contiguous: thread k holds spans t*kPlanTile + 8k .. +7).
+__global__ __launch_bounds__(kPlanThreads) void k_plan_tiles(const uint64_t *nunit, const uint8_t *fast, uint64_t n,
+                                                            PlanSum *tile_sum) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
+    __shared__ PlanSum sh[kPlanThreads / 64];
+    const uint64_t ntiles = (n + kPlanTile - 1) / kPlanTile;
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t i0 = t * kPlanTile + (uint64_t)threadIdx.x * kPlanPer;
+        PlanSum s{0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t k = 0; k < kPlanPer; ++k) s = plan_add(s, plan_at(nunit, fast, n, i0 + k));
+        PlanSum tot;
+        (void)block_scan_excl(s, sh, &tot);
+        if (threadIdx.x == 0) tile_sum[t] = tot;
+    }
+}
+
+// Exclusive scan of the ntiles tile sums by one workgroup; tile_pre[ntiles] =
+// the grand total (units, blocks and fast spans of the whole batch).
+__global__ __launch_bounds__(kPlanThreads) void k_plan_scan(const PlanSum *tile_sum, uint64_t ntiles,
+                                                           PlanSum *tile_pre) {
+    MCRC_VGPR_FLOOR();
+    __shared__ PlanSum sh[kPlanThreads / 64];
+    PlanSum carry{0, 0, 0, 0};
+    for (uint64_t t0 = 0; t0 < ntiles; t0 += kPlanThreads) {
+        const uint64_t t = t0 + threadIdx.x;
+        PlanSum tot;
+        const PlanSum ex = block_scan_excl(t < ntiles ? tile_sum[t] : PlanSum{0, 0, 0, 0}, sh, &tot);
+        if (t < ntiles) tile_pre[t] = plan_add(carry, ex);
+        carry = plan_add(carry, tot);
+    }
+    if (threadIdx.x == 0) tile_pre[ntiles] = carry;
+}
+
+// Exclusive scan of m 32-bit counts by one workgroup (the device page walk:
+// the index of each wbuf's first item; a few thousand wbufs per call).
+// out[m] = the total.
+__global__ __launch_bounds__(1024) void k_scan32(const uint32_t *in, uint64_t m, uint32_t *out) {
+    MCRC_VGPR_FLOOR();
+    __shared__ uint32_t sh[16];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t carry = 0;
+    for (uint64_t i0 = 0; i0 < m; i0 += 1024) {
+        const uint64_t i = i0 + threadIdx.x;
+        const uint32_t v = i < m ? in[i] : 0u;
+        uint32_t inc = v;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += o;
+        }
+        if (lane == 63) sh[w] = inc;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (uint32_t k = 0; k < 16; ++k) {
+            before += k < w ? sh[k] : 0u;
+            all += sh[k];
+        }
+        __syncthreads();
+        if (i < m) out[i] = carry + before + inc - v;
+        carry += all;
+    }
+    if (threadIdx.x == 0) out[m] = carry;
+}
+
+// Write the unit records of span i at its units prefix.  Spans whose units would pass
 // `cap` (possible only when spans overlap) are listed in `whole` and processed
 // as one unit each by a second pass; *nvalid = records written before the
 // first such span (zeroed by the caller: none fit).  Spans of more than kExpandInline segments are listed in `big`
@@ -1044,11 +1160,11 @@ struct Balance {
     uint64_t gm;   // groups with blocks: boundaries 1 .. gm - 1
 };
 
-__device__ __forceinline__ Balance balance_of(const uint64_t *nunit, const uint64_t *prefix, uint64_t n,
-                                              uint32_t groups, uint32_t *starts) {
+// (total: the batch's grand total from k_plan_scan)
+__device__ __forceinline__ Balance balance_of(const PlanSum *total, uint64_t n, uint32_t groups, uint32_t *starts) {
     Balance b{starts, 1, 0};
     if (starts && n) {
-        const uint64_t t = (prefix[n - 1] + nunit[n - 1]) >> 32;
+        const uint64_t t = total->blocks;
         b.per = max((t + groups - 1) / groups, (uint64_t)1);
         b.gm = (t + b.per - 1) / b.per;
     }
@@ -1079,50 +1195,74 @@ __device__ __forceinline__ void put_unit(UnitRec *units, const Balance &b, uint6
     units[idx] = unit_piece(r, k0, nb);
 }
 
-__global__ void k_expand(const uint8_t *base, const uint64_t *nunit, const uint64_t *prefix, const uint4 *irec,
-                         uint64_t n, UnitRec *units, uint64_t cap, uint32_t *nvalid, UnitRec *whole,
-                         uint32_t *nwhole, uint32_t *big, uint32_t *nbig, uint32_t groups, uint32_t *starts) {
+// Per tile (kPlanTile spans, thread-contiguous as k_plan_tiles): the tile's
+// prefix from k_plan_scan plus the exclusive scan inside the tile places every
+// span's units (p0), first block (b0) and, for a one-block span, its slot in
+// the compacted list fastidx (k_blocks).
+__global__ __launch_bounds__(kPlanThreads) void k_expand(const uint8_t *base, const uint64_t *nunit, const uint8_t *fast,
+                                                        const PlanSum *tile_pre, const uint4 *irec, uint64_t n,
+                                                        UnitRec *units, uint64_t cap, uint32_t *nvalid, UnitRec *whole,
+                                                        uint32_t *nwhole, uint4 *big, uint32_t *nbig, uint32_t *fastidx,
+                                                        uint32_t groups, uint32_t *starts) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
-    const Balance bal = balance_of(nunit, prefix, n, groups, starts);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t pk = prefix[i], ck = nunit[i];
-        const uint64_t p0 = (uint32_t)pk, ns = (uint32_t)ck, b0 = pk >> 32;
-        const uint4 r = irec[i];
-        const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
-        const bool sane = !(r.y & kInsane);
-        if (p0 + ns <= cap) {
-            const uint32_t s0 = first_seg(base + off, r.z, (uint32_t)ns);
-            if (ns > kExpandInline) {
-                big[atomicAdd(nbig, 1u)] = (uint32_t)i;
-            } else {
-                uint64_t bs = b0;
-                for (uint32_t s = 0; s < ns; ++s) {
-                    const UnitRec u = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, s0 + s);
-                    put_unit(units, bal, p0 + s, bs, u);
-                    bs += u.b.z >> 8;
+    __shared__ PlanSum sh[kPlanThreads / 64];
+    const uint64_t ntiles = (n + kPlanTile - 1) / kPlanTile;
+    const Balance bal = balance_of(tile_pre + ntiles, n, groups, starts);
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint64_t i0 = t * kPlanTile + (uint64_t)threadIdx.x * kPlanPer;
+        uint64_t ck[kPlanPer];
+        uint8_t fk[kPlanPer];
+        PlanSum s{0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t k = 0; k < kPlanPer; ++k) {
+            ck[k] = i0 + k < n ? nunit[i0 + k] : 0ull;
+            fk[k] = i0 + k < n ? fast[i0 + k] : (uint8_t)0;
+            s = plan_add(s, plan_of(ck[k], fk[k]));
+        }
+        PlanSum tot;
+        PlanSum pre = plan_add(tile_pre[t], block_scan_excl(s, sh, &tot));
+        for (uint32_t k = 0; k < kPlanPer && i0 + k < n; ++k) {
+            const uint64_t i = i0 + k;
+            const uint64_t p0 = pre.units, ns = (uint32_t)ck[k], b0 = pre.blocks;
+            if (fk[k]) fastidx[pre.fast] = (uint32_t)i;
+            const uint4 r = irec[i];
+            const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
+            const bool sane = !(r.y & kInsane);
+            if (p0 + ns <= cap) {
+                const uint32_t s0 = first_seg(base + off, r.z, (uint32_t)ns);
+                if (ns > kExpandInline) {
+                    big[atomicAdd(nbig, 1u)] = make_uint4((uint32_t)i, (uint32_t)p0, (uint32_t)b0, (uint32_t)(b0 >> 32));
+                } else {
+                    uint64_t bs = b0;
+                    for (uint32_t sg = 0; sg < ns; ++sg) {
+                        const UnitRec u = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, s0 + sg);
+                        put_unit(units, bal, p0 + sg, bs, u);
+                        bs += u.b.z >> 8;
+                    }
                 }
+                // the last span whose units fit: the record count
+                if (i + 1 == n || p0 + ns + (uint32_t)nunit[i + 1] > cap)
+                    *nvalid = (uint32_t)(p0 + ns + cuts_before(bal, b0 + (ck[k] >> 32)));
+            } else {
+                // (one unit with the span's head rule: the same grid, so the same G1)
+                whole[atomicAdd(nwhole, 1u)] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, kWhole);
             }
-            // the last span whose units fit: the record count
-            if (i + 1 == n || (uint64_t)(uint32_t)prefix[i + 1] + (uint32_t)nunit[i + 1] > cap)
-                *nvalid = (uint32_t)(p0 + ns + cuts_before(bal, b0 + (ck >> 32)));
-        } else {
-            // (one unit with the span's head rule: the same grid, so the same G1)
-            whole[atomicAdd(nwhole, 1u)] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, kWhole);
+            pre = plan_add(pre, plan_of(ck[k], fk[k]));
         }
     }
 }
 
-__global__ void k_expand_big(const uint8_t *base, const uint64_t *nunit, const uint64_t *prefix, const uint4 *irec,
-                             UnitRec *units, const uint32_t *big, const uint32_t *nbig, uint64_t n, uint32_t groups,
+// big[b] = {span, p0, b0 (lo, hi)} from k_expand.
+__global__ void k_expand_big(const uint8_t *base, const uint64_t *nunit, const PlanSum *total, const uint4 *irec,
+                             UnitRec *units, const uint4 *big, const uint32_t *nbig, uint64_t n, uint32_t groups,
                              uint32_t *starts) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
-    const Balance bal = balance_of(nunit, prefix, n, groups, starts);
+    const Balance bal = balance_of(total, n, groups, starts);
     const uint32_t nb = *nbig;
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        const uint32_t i = big[b];
-        const uint64_t pk = prefix[i];
-        const uint64_t p0 = (uint32_t)pk, b0 = pk >> 32;
+        const uint4 e = big[b];
+        const uint32_t i = e.x;
+        const uint64_t p0 = e.y, b0 = e.z | ((uint64_t)e.w << 32);
         const uint32_t ns = (uint32_t)nunit[i];
         const uint4 r = irec[i];
         const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);

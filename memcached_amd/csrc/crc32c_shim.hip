@@ -5,7 +5,6 @@
 // (crc32c.c:47, :266-275, :507-513); the batch symbols replace loops of those
 // calls in storage.c / proxy_internal.c (see include/crc32c_batch.h).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -90,7 +89,7 @@ struct Device {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};  // host-batch pipeline slots
     std::mutex mu;              // serialises the entry points that use the scratch below
-    Queue *queue = nullptr;     // coalescing queue (crc32c_batch_submit), created on first use
+    std::atomic<Queue *> queue{nullptr};  // coalescing queue (crc32c_batch_submit), created on first use
     // Shared device scratch (plan buffers, nbad, walk buffers) is owned in
     // stream order: a launch on stream B waits for the last use on stream A.
     hipEvent_t busy = nullptr;
@@ -115,17 +114,16 @@ struct Device {
     uint32_t *hlens[2] = {nullptr, nullptr}, *hcin[2] = {nullptr, nullptr}, *hout[2] = {nullptr, nullptr};
     uint64_t slot_items = 0;
     // work-unit planning for long / variable spans (grow-only)
-    uint64_t *nunit = nullptr, *prefix = nullptr;  // per span: units | blocks << 32, and its exclusive scan
+    uint64_t *nunit = nullptr;  // per span: units | blocks << 32
+    mcrc_dev::PlanSum *tile_sum = nullptr, *tile_pre = nullptr;  // per kPlanTile spans: sums, exclusive scan (+ total)
     uint32_t *span_acc = nullptr, *counters = nullptr;
     uint32_t *starts = nullptr;  // balanced plan: first record of each span-kernel group (groups + 1)
     uint32_t *segpow = nullptr;  // rows x^i * x^(8*4096*k): k < 256, then k = 256 j
     mcrc_dev::UnitRec *units = nullptr, *whole = nullptr;
     uint4 *irec = nullptr;  // per-span record written by k_count
     uint8_t *fast = nullptr;     // per span: its unit is one whole block (k_blocks takes it)
-    uint32_t *fastidx = nullptr; // the fast spans' indices, compacted (hipcub DeviceSelect)
-    uint32_t *big = nullptr;  // spans expanded by k_expand_big
-    void *scan_tmp = nullptr;
-    size_t scan_tmp_bytes = 0;
+    uint32_t *fastidx = nullptr; // the fast spans' indices, compacted (k_expand)
+    uint4 *big = nullptr;  // spans expanded by k_expand_big: {span, p0, b0}
     uint64_t plan_items = 0, plan_units = 0;
     // grow-only scratch for the page walk and staged item batches
     struct Scratch {
@@ -335,7 +333,8 @@ uint32_t span_groups(const Device &d) { return (uint32_t)d.cus * (mcrc_dev::kSpa
 int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
     if (d.plan_items < n) {
         (void)hipFree(d.nunit);
-        (void)hipFree(d.prefix);
+        (void)hipFree(d.tile_sum);
+        (void)hipFree(d.tile_pre);
         (void)hipFree(d.whole);
         (void)hipFree(d.irec);
         (void)hipFree(d.span_acc);
@@ -343,23 +342,15 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
         (void)hipFree(d.fast);
         (void)hipFree(d.fastidx);
         d.plan_items = 0;
-        if (hipMalloc(&d.nunit, n * 8) != hipSuccess || hipMalloc(&d.prefix, n * 8) != hipSuccess ||
+        const uint64_t ntiles = (n + mcrc_dev::kPlanTile - 1) / mcrc_dev::kPlanTile;
+        if (hipMalloc(&d.nunit, n * 8) != hipSuccess ||
+            hipMalloc(&d.tile_sum, ntiles * sizeof(mcrc_dev::PlanSum)) != hipSuccess ||
+            hipMalloc(&d.tile_pre, (ntiles + 1) * sizeof(mcrc_dev::PlanSum)) != hipSuccess ||
             hipMalloc(&d.whole, n * sizeof(mcrc_dev::UnitRec)) != hipSuccess ||
             hipMalloc(&d.irec, n * sizeof(uint4)) != hipSuccess || hipMalloc(&d.span_acc, n * 4) != hipSuccess ||
-            hipMalloc(&d.big, n * 4) != hipSuccess || hipMalloc(&d.fast, n) != hipSuccess ||
+            hipMalloc(&d.big, n * sizeof(uint4)) != hipSuccess || hipMalloc(&d.fast, n) != hipSuccess ||
             hipMalloc(&d.fastidx, n * 4) != hipSuccess)
             return CRC32C_ENOMEM;
-        size_t need = 0, need2 = 0;
-        if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, d.nunit, d.prefix, (int)n) != hipSuccess ||
-            hipcub::DeviceSelect::Flagged(nullptr, need2, hipcub::CountingInputIterator<uint32_t>(0), d.fast,
-                                          d.fastidx, d.counters, (int)n) != hipSuccess)
-            return CRC32C_EHIP;
-        need = std::max(need, need2);
-        if (need > d.scan_tmp_bytes) {
-            (void)hipFree(d.scan_tmp);
-            if (hipMalloc(&d.scan_tmp, need) != hipSuccess) return CRC32C_ENOMEM;
-            d.scan_tmp_bytes = need;
-        }
         d.plan_items = n;
     }
     if (d.plan_units < cap) {
@@ -515,22 +506,30 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     const uint64_t cap = plan_cap(a);
     int rc = ensure_plan(d, n, cap);
     if (rc) return rc;
-    uint32_t *nvalid = d.counters, *nwhole = d.counters + 1, *nbig = d.counters + 2, *nfast = d.counters + 3;
+    uint32_t *nvalid = d.counters, *nwhole = d.counters + 1, *nbig = d.counters + 2;
     HIP_OK(hipMemsetAsync(nvalid, 0, 12, st));  // nvalid, nwhole, nbig
     if (kSpanBalance) HIP_OK(hipMemsetAsync(d.starts, 0xff, (span_groups(d) + 1) * 4, st));
     a.span_acc = d.span_acc;
     if (!path.counted)
         hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nunit, d.irec, d.fast);
-    size_t tmp = d.scan_tmp_bytes;
-    HIP_OK(hipcub::DeviceScan::ExclusiveSum(d.scan_tmp, tmp, d.nunit, d.prefix, (int)n, st));
-    tmp = d.scan_tmp_bytes;
-    HIP_OK(hipcub::DeviceSelect::Flagged(d.scan_tmp, tmp, hipcub::CountingInputIterator<uint32_t>(0), d.fast,
-                                         d.fastidx, nfast, (int)n, st));
+    // prefix sums of the plan (units, blocks, one-block spans): tile sums, one
+    // workgroup over them, then each tile rescanned where k_expand uses it
+    const uint64_t ntiles = (n + mcrc_dev::kPlanTile - 1) / mcrc_dev::kPlanTile;
+    const int gt = (int)std::min<uint64_t>(ntiles, 4096);
+    hipLaunchKernelGGL(mcrc_dev::k_plan_tiles, dim3(gt), dim3(mcrc_dev::kPlanThreads), 0, st,
+                       (const uint64_t *)d.nunit, (const uint8_t *)d.fast, n, d.tile_sum);
+    hipLaunchKernelGGL(mcrc_dev::k_plan_scan, dim3(1), dim3(mcrc_dev::kPlanThreads), 0, st,
+                       (const mcrc_dev::PlanSum *)d.tile_sum, ntiles, d.tile_pre);
+    const mcrc_dev::PlanSum *total = d.tile_pre + ntiles;
+    const uint32_t *nfast = &d.tile_pre[ntiles].fast;
     uint32_t *const starts = kSpanBalance ? d.starts : nullptr;
-    hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(g1), dim3(256), 0, st, a.base, d.nunit, d.prefix, d.irec, n, d.units,
-                       cap, nvalid, d.whole, nwhole, d.big, nbig, span_groups(d), starts);
-    hipLaunchKernelGGL(mcrc_dev::k_expand_big, dim3(1024), dim3(256), 0, st, a.base, d.nunit, d.prefix, d.irec,
-                       d.units, d.big, nbig, n, span_groups(d), starts);
+    hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(gt), dim3(mcrc_dev::kPlanThreads), 0, st, a.base,
+                       (const uint64_t *)d.nunit, (const uint8_t *)d.fast, (const mcrc_dev::PlanSum *)d.tile_pre,
+                       (const uint4 *)d.irec, n, d.units, cap, nvalid, d.whole, nwhole, d.big, nbig, d.fastidx,
+                       span_groups(d), starts);
+    hipLaunchKernelGGL(mcrc_dev::k_expand_big, dim3(1024), dim3(256), 0, st, a.base, (const uint64_t *)d.nunit,
+                       total, (const uint4 *)d.irec, d.units, (const uint4 *)d.big, (const uint32_t *)nbig, n,
+                       span_groups(d), starts);
     mcrc_dev::SpanArgs u = a;
     u.units = d.units;
     u.nunits = nvalid;
@@ -675,13 +674,18 @@ bool device_range_ok(const void *p, uint64_t bytes) {
     return skip <= size && bytes <= size - skip;
 }
 
-bool is_pinned_or_device(const void *p) {
+const uint8_t *device_view_range(const void *p, uint64_t bytes);
+
+// [p, p + bytes) can be the source of one DMA as it lies: device or managed
+// memory, or host memory page-locked over the whole range.
+bool is_pinned_or_device(const void *p, uint64_t bytes) {
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
-    return at.type == hipMemoryTypeHost || at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+    if (at.type == hipMemoryTypeHost) return device_view_range(p, bytes) != nullptr;
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
 }
 
 // The address a kernel reads host memory p at, when p is page-locked and
@@ -700,6 +704,32 @@ const uint8_t *device_view(const void *p) {
         return nullptr;
     }
     return (const uint8_t *)dp;
+}
+
+// The device address of the whole host range [p, p + bytes) when every byte
+// of it is page-locked and mapped as one contiguous range, else nullptr (the
+// caller then stages the batch).  A caller may have registered only part of
+// an arena, or pass a base_bytes past the end of its hipHostMalloc buffer: a
+// kernel reading such a range in place would page-fault.  The runtime's
+// record of the allocation or registration holding p must cover the range;
+// where the runtime cannot describe it, both ends must map, to addresses
+// bytes - 1 apart.
+const uint8_t *device_view_range(const void *p, uint64_t bytes) {
+    const uint8_t *dv = device_view(p);
+    if (!dv || bytes <= 1) return dv;
+    const uint8_t *h = (const uint8_t *)p;
+    hipDeviceptr_t lo = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&lo, &size, (hipDeviceptr_t)p) == hipSuccess && lo) {
+        // (the base comes back as the host or as the device address of the range)
+        for (const uint8_t *q : {h, dv}) {
+            const uint8_t *b = (const uint8_t *)lo;
+            if (q >= b && (uint64_t)(q - b) <= size) return bytes <= size - (uint64_t)(q - b) ? dv : nullptr;
+        }
+        return nullptr;
+    }
+    (void)hipGetLastError();
+    return device_view(h + bytes - 1) == dv + (bytes - 1) ? dv : nullptr;
 }
 
 uint64_t span_off(const crc32c_spans &s, uint64_t i) { return s.offsets ? s.offsets[i] : i * s.stride; }
@@ -788,7 +818,7 @@ int run_host_batch(Device &d, const crc32c_spans &s) {
             d.release(d.stream);
         }
     } guard{d};
-    const bool src_pinned = is_pinned_or_device(s.base);
+    const bool src_pinned = is_pinned_or_device(s.base, s.base_bytes);
     const uint8_t *src = (const uint8_t *)s.base;
     uint64_t pend_k0[2] = {0, 0}, pend_n[2] = {0, 0};  // results waiting in hout[slot]
     auto drain = [&](int k) -> int {
@@ -958,7 +988,7 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
     if (!d->grow_pinned(kPinOffs, n * 8, &h_offs, &v_offs) || !d->grow_pinned(kPinOk, n, &h_ok, &v_ok))
         return CRC32C_ENOMEM;
     memcpy(h_offs, item_offsets, n * 8);
-    const uint8_t *mapped = device_view(base);
+    const uint8_t *mapped = device_view_range(base, base_bytes);
     // stamp results come back as CRCs (scattered into the caller's images
     // here) unless the kernel stamps the caller's page-locked buffer itself
     const bool crcs_back = MODE == 2 && !(path.small && mapped);
@@ -1021,6 +1051,10 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
 struct crc32c_job {
     crc32c_spans s;
     unsigned flags = 0;
+    // CRC32C_DEVICE jobs: recorded on the submitter's default stream, waited
+    // for by the queue's stream before the job runs (work the caller queued on
+    // the default stream, e.g. the copy filling the spans, stays ordered first)
+    hipEvent_t after = nullptr;
     const uint8_t *dbase = nullptr;  // coalesced jobs: the device view of s.base
     bool coalesce = false;
     int rc = CRC32C_OK;
@@ -1071,10 +1105,23 @@ struct Queue {
         }
         HIP_OK(hipMalloc(&dnbad, sizeof(unsigned long long)));
         HIP_OK(hipMemset(dnbad, 0, sizeof(unsigned long long)));
-        // the dispatcher lives as long as the process (never joined: the queue
-        // is not freed, and at exit the thread is blocked on cv_work)
-        std::thread([this] { run(); }).detach();
+        // the dispatcher runs until process exit: an atexit hook (registered
+        // after the HIP runtime initialised, so it runs before HIP's static
+        // destructors) stops it once the queue has drained and joins it
+        worker = std::thread([this] { run(); });
         return CRC32C_OK;
+    }
+
+    std::thread worker;
+    bool stop = false;  // (under mu)
+
+    void shutdown() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv_work.notify_one();
+        if (worker.joinable()) worker.join();
     }
 
     void submit(crc32c_job *j) {
@@ -1158,7 +1205,15 @@ struct Queue {
 
     int run_solo(crc32c_job *j) {
         solo.fetch_add(1, std::memory_order_relaxed);
-        if (j->flags & CRC32C_DEVICE) return device_batch(*d, j->s, j->flags & ~(unsigned)CRC32C_ASYNC, st);
+        if (j->flags & CRC32C_DEVICE) {
+            if (j->after) {
+                const hipError_t e = hipStreamWaitEvent(st, j->after, 0);
+                (void)hipEventDestroy(j->after);
+                j->after = nullptr;
+                if (e != hipSuccess) return CRC32C_EHIP;
+            }
+            return device_batch(*d, j->s, j->flags & ~(unsigned)CRC32C_ASYNC, st);
+        }
         return run_host_batch(*d, j->s);
     }
 
@@ -1171,7 +1226,10 @@ struct Queue {
             crc32c_job *solo_job = nullptr;
             {
                 std::unique_lock<std::mutex> lk(mu);
-                if (busy.jobs.empty()) cv_work.wait(lk, [&] { return !pending.empty(); });
+                if (busy.jobs.empty()) {
+                    cv_work.wait(lk, [&] { return !pending.empty() || stop; });
+                    if (pending.empty()) return;  // stop, and nothing in flight
+                }
                 if (!pending.empty() && !pending.front()->coalesce) {
                     solo_job = pending.front();
                     pending.pop_front();
@@ -1196,16 +1254,25 @@ struct Queue {
     }
 };
 
+// Every device's dispatcher stops (after its pending jobs) at process exit.
+void stop_queues() {
+    for (auto &d : g_devs)
+        if (Queue *q = d->queue.load(std::memory_order_acquire)) q->shutdown();
+}
+
 int queue_of(Device &d, Queue **out) {
     static std::mutex mu;
+    static bool hooked = false;
     std::lock_guard<std::mutex> lk(mu);
-    if (!d.queue) {
-        Queue *q = new Queue();
+    Queue *q = d.queue.load(std::memory_order_acquire);
+    if (!q) {
+        q = new Queue();
         const int rc = q->init(d);
         if (rc) return rc;  // (a partly initialised queue is leaked, not reused)
-        d.queue = q;
+        if (!hooked) hooked = std::atexit(stop_queues) == 0;
+        d.queue.store(q, std::memory_order_release);
     }
-    *out = d.queue;
+    *out = q;
     return CRC32C_OK;
 }
 
@@ -1222,14 +1289,22 @@ int make_job(const crc32c_spans &s, unsigned flags, crc32c_job **out) {
     j->s = s;
     j->flags = flags & ~(unsigned)CRC32C_ASYNC;
     j->q = q;
-    if (!(flags & CRC32C_DEVICE)) {
+    if (flags & CRC32C_DEVICE) {
+        // order the job after the submitter's default stream (its work so far)
+        if (hipEventCreateWithFlags(&j->after, hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(j->after, nullptr) != hipSuccess) {
+            if (j->after) (void)hipEventDestroy(j->after);
+            delete j;
+            return CRC32C_EHIP;
+        }
+    } else {
         if (!host_spans_ok(s)) {
             delete j;
             return CRC32C_EINVAL;
         }
         bool short_spans = s.n >= 1 && s.n <= mcrc_dev::kSmallMax;
         for (uint64_t i = 0; short_spans && i < s.n; ++i) short_spans = span_len(s, i) <= kQueueSpanMax;
-        if (short_spans && (j->dbase = device_view(s.base)) != nullptr) j->coalesce = true;
+        if (short_spans && (j->dbase = device_view_range(s.base, s.base_bytes)) != nullptr) j->coalesce = true;
     }
     *out = j;
     return CRC32C_OK;
@@ -1313,7 +1388,7 @@ int crc32c_queue_stats(uint64_t *launches, uint64_t *spans, uint64_t *jobs, uint
     Device *d = nullptr;
     const int rc = current_device(&d);
     if (rc) return rc;
-    const Queue *q = d->queue;
+    const Queue *q = d->queue.load(std::memory_order_acquire);
     if (launches) *launches = q ? q->launches.load() : 0;
     if (spans) *spans = q ? q->spans.load() : 0;
     if (jobs) *jobs = q ? q->jobs.load() : 0;
@@ -1447,11 +1522,8 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     }
     // counts of nw wbufs and a zero: the exclusive scan's last entry is the total
     uint32_t *cnt = (uint32_t *)d->grow(kScrWalkCnt, (nw + 1) * 4);
-    uint32_t *prefix = (uint32_t *)d->grow(kScrWalkPrefix, (nw + 1) * 4);
-    size_t tmp = 0;
-    HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, prefix, (int)nw + 1));
-    void *scan = d->grow(kScrWalkScan, tmp);
-    if (!cnt || !prefix || !scan) return CRC32C_ENOMEM;
+    uint32_t *prefix = (uint32_t *)d->grow(kScrWalkPrefix, (nw + 2) * 4);
+    if (!cnt || !prefix) return CRC32C_ENOMEM;
     mcrc_dev::SpanArgs a{};
     a.base = dbase;
     a.base_bytes = base_bytes;
@@ -1468,7 +1540,7 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     wo.cnt = cnt;
     HIP_OK(hipMemsetAsync(cnt + nw, 0, 4, st));
     hipLaunchKernelGGL(mcrc_dev::k_walk<false>, dim3(gw), bw, 0, st, a, nw, wo);
-    HIP_OK(hipcub::DeviceScan::ExclusiveSum(scan, tmp, cnt, prefix, (int)nw + 1, st));
+    hipLaunchKernelGGL(mcrc_dev::k_scan32, dim3(1), dim3(1024), 0, st, (const uint32_t *)cnt, nw + 1, prefix);
     uint32_t total = 0;
     HIP_OK(hipMemcpyAsync(&total, prefix + nw, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));

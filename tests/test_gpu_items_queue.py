@@ -482,3 +482,62 @@ def test_k5_verify_stamp_and_walk_with_fallback(torch):
     torch.cuda.synchronize()
     assert nbad == 0 and bool(ok.all())
     np.testing.assert_array_equal(dz.cpu().numpy(), clean)
+
+
+def test_partly_registered_buffer_is_staged_not_read_in_place(torch):
+    """A caller that page-locks only part of a buffer (crc32c_host_register of
+    the first half of an arena) and passes spans or item images in the other
+    half: the library must not read (or stamp) the range in place, which would
+    page-fault the GPU; it stages those batches instead.  A fully registered
+    buffer still takes the zero-copy path (coalesced by the queue)."""
+    import mmap
+    rng = np.random.default_rng(77)
+    size = 4 << 20
+    mm = mmap.mmap(-1, size)  # page-aligned, pageable
+    arena = np.frombuffer(mm, dtype=np.uint8)
+    arena[:] = rng.integers(0, 256, size, dtype=np.uint8)
+    half = size // 2
+    _lib.check(_lib.lib.crc32c_host_register(ctypes.c_void_p(arena.ctypes.data), ctypes.c_size_t(half)), "register")
+    try:
+        # spans on both sides of the registered boundary, through the queue
+        n = 64
+        lens = rng.integers(1, 60000, n).astype(np.uint32)
+        offs = np.array([int(rng.integers(0, size - int(x))) for x in lens], np.uint64)
+        offs[:8] = half - 100  # straddling the boundary
+        offs[8:16] = size - lens[8:16]  # wholly in the unregistered half
+        cin = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+        want = oracle.batch(arena, offs, lens, cin)
+        l0, s0, j0, q0 = mc.queue_stats()
+        out = np.empty(n, np.uint32)
+        sp = _lib.Spans(arena.ctypes.data, size, offs.ctypes.data, 0, lens.ctypes.data, 0, cin.ctypes.data,
+                        out.ctypes.data, n)
+        _lib.check(_lib.lib.crc32c_batch_wait(_submit(sp)), "wait")
+        np.testing.assert_array_equal(out, want)
+        l1, s1, j1, q1 = mc.queue_stats()
+        assert q1 - q0 == 1 and j1 == j0  # run alone (staged), not coalesced in place
+        np.testing.assert_array_equal(mc.batch(arena, offsets=offs, lens=lens, crc_in=cin), want)
+        # the registered half alone is read in place (coalesced)
+        inner = offs[16:][offs[16:] + lens[16:] <= half]
+        il = lens[16:][offs[16:] + lens[16:] <= half]
+        if inner.size:
+            out2 = np.empty(inner.size, np.uint32)
+            sp2 = _lib.Spans(arena.ctypes.data, half, inner.ctypes.data, 0, il.ctypes.data, 0, None,
+                             out2.ctypes.data, inner.size)
+            _lib.check(_lib.lib.crc32c_batch_wait(_submit(sp2)), "wait")
+            np.testing.assert_array_equal(out2, oracle.batch(arena, inner, il))
+            l2, s2, j2, q2 = mc.queue_stats()
+            assert j2 - j1 == 1 and q2 == q1
+        # item images packed into a wbuf that straddles the boundary: stamp and verify
+        wbuf = 1 << 20
+        items_buf, ioffs = _pages(rng, 300, wbuf, 4, max_value=2500)
+        lo = half - wbuf // 2
+        view = arena[lo:lo + items_buf.size]
+        view[:] = items_buf
+        layout.store_crcs(view, ioffs, np.zeros(ioffs.size, np.uint32))
+        ok, nbad = mc.stamp_items(view, ioffs, region_bytes=wbuf)
+        assert nbad == 0 and ok.all()
+        np.testing.assert_array_equal(_stored(view, ioffs), _crcs(view, ioffs, 4))
+        ok, nbad = mc.verify_items(view, ioffs, region_bytes=wbuf)
+        assert nbad == 0 and ok.all()
+    finally:
+        _lib.check(_lib.lib.crc32c_host_unregister(ctypes.c_void_p(arena.ctypes.data)), "unregister")
