@@ -101,6 +101,27 @@ constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 constexpr uint32_t kNibShiftBytes = 20 * 1024;
 constexpr uint32_t nib_set(uint32_t t0) { return t0 == kAuxShift0 ? 0u : t0 == kAuxShift1 ? 1u : 2u; }
 
+// MCRC_NIB == 2: level 0 of the lane tree folded into the chains as well.
+// Every row's last step reads nibble tables: row r of an even lane ends with
+// M_{(3-r)*1024 + 32} (its odd neighbour's 32 bytes follow), of an odd lane
+// with M_{(3-r)*1024}, so level 0 is a plain XOR of the two lanes.  Set
+// (r, parity p): table k (nibble k) at kNibShiftBytes + 1024 r + 128 k + 64 p
+// -- even lanes' tables in banks 0-15, odd lanes' in 16-31: still one entry
+// per bank per instruction.
+__device__ __forceinline__ uint32_t step4_last_nib2(uint32_t x, uint32_t r, uint32_t par64x4) {
+    uint32_t lo = __builtin_amdgcn_alignbit(x, x, 30), hi = __builtin_amdgcn_alignbit(x, x, 2);
+    asm volatile("" : "+v"(lo), "+v"(hi));
+    // nibble * 4 in bits 2..5 of every byte, the lane's parity in bit 6
+    lo = (lo & 0x3c3c3c3cu) | par64x4;
+    hi = (hi & 0x3c3c3c3cu) | par64x4;
+    const uint32_t b = kNibShiftBytes + 1024u * r;
+    return xor3(xor3(lds_ld(b + (lo & 0xffu)), lds_ld(b + 128 + (hi & 0xffu)), lds_ld(b + 256 + ((lo >> 8) & 0xffu))),
+                xor3(lds_ld(b + 384 + ((hi >> 8) & 0xffu)), lds_ld(b + 512 + ((lo >> 16) & 0xffu)),
+                     lds_ld(b + 640 + ((hi >> 16) & 0xffu))),
+                lds_ld(b + 768 + (lo >> 24))) ^
+           lds_ld(b + 896 + (hi >> 24));
+}
+
 // Last slice-by-4 step of a row chain through the shifted tables t0..t0+3:
 // returns M_shift(T3[x0] ^ T2[x1] ^ T1[x2] ^ T0[x3]).
 __device__ __forceinline__ uint32_t step4_last_shifted(uint32_t x, uint32_t t0) {
@@ -148,6 +169,11 @@ template <int K = 0>
 __device__ __forceinline__ uint32_t group_reduce32_dpp(uint32_t v, uint32_t lane) {
     if constexpr (K == 5) {
         return v;
+#if MCRC_NIB == 2
+    } else if constexpr (K == 0) {
+        const uint32_t x = lane_down<0>(v);  // (M_32 is in the even lanes' last steps)
+        return group_reduce32_dpp<1>((lane & 1u) == 0u ? v ^ x : v, lane);
+#endif
     } else {
         const uint32_t x = lane_down<K>(v);
         if ((lane & ((2u << K) - 1u)) == 0) v = xor3(Step<4>::aux(kAuxTree + 4 * K, v & 0xffu) ^ x,
@@ -162,6 +188,9 @@ __device__ __forceinline__ uint32_t group_reduce32_dpp(uint32_t v, uint32_t lane
 template <int K>
 __device__ __forceinline__ uint32_t reduce_level(uint32_t v, bool on) {
     const uint32_t x = lane_down<K>(v);
+#if MCRC_NIB == 2
+    if constexpr (K == 0) return on ? v ^ x : v;  // (M_32 is in the even lanes' last steps)
+#endif
     if (on) v = xor3(Step<4>::aux(kAuxTree + 4 * K, v & 0xffu) ^ x, Step<4>::aux(kAuxTree + 4 * K + 1, (v >> 8) & 0xffu),
                      Step<4>::aux(kAuxTree + 4 * K + 2, (v >> 16) & 0xffu)) ^
                 Step<4>::aux(kAuxTree + 4 * K + 3, v >> 24);

@@ -78,6 +78,9 @@ __device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &
     constexpr int N = 4 * Q;  // dwords per chain
     constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};
     uint32_t x[4];
+#if MCRC_NIB == 2
+    const uint32_t par = (c.lane4 & 4u) ? 0x40404040u : 0u;  // odd lane
+#endif
 #pragma unroll
     for (int r = 0; r < 4; ++r) x[r] = it.d[r][0].x;
 #pragma unroll
@@ -87,7 +90,11 @@ __device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &
             if (i + 1 < N) {
                 x[r] = step4_next(x[r], dw4(it.d[r][(i + 1) >> 2], (i + 1) & 3), c);
             } else {
+#if MCRC_NIB == 2
+                x[r] = step4_last_nib2(x[r], r, par);
+#else
                 x[r] = r < 3 ? step4_last_shifted(x[r], kShift[r]) : step4_next(x[r], 0u, c);
+#endif
             }
         }
     }
@@ -289,7 +296,12 @@ struct SpanArgs {
     // workgroup moves *nbad to this pinned host word and zeroes *nbad and *done
     unsigned long long *host_nbad;
     uint32_t *done;            // finished workgroups
+    // planned path over a list whose length is known only on the device (K5's
+    // fallback list): n spans at most, *dn of them (nullptr: n)
+    const uint32_t *dn;
 };
+
+__device__ __forceinline__ uint64_t span_count(const SpanArgs &a) { return a.dn ? (uint64_t)*a.dn : a.n; }
 
 struct ItemDesc {
     const uint8_t *p;
@@ -744,6 +756,9 @@ template <int NS>
 __device__ __forceinline__ uint32_t block_value(const BlockWin &w, const LaneCtx &c) {
     constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};
     uint32_t x[4];
+#if MCRC_NIB == 2
+    const uint32_t par = (c.lane4 & 4u) ? 0x40404040u : 0u;  // odd lane
+#endif
 #pragma unroll
     for (int r = NS; r < 4; ++r) x[r] = w.v[r][0].x;
 #pragma unroll
@@ -753,7 +768,11 @@ __device__ __forceinline__ uint32_t block_value(const BlockWin &w, const LaneCtx
             if (i + 1 < 8) {
                 x[r] = step4_next(x[r], dw4(w.v[r][(i + 1) >> 2], (i + 1) & 3), c);
             } else {
+#if MCRC_NIB == 2
+                x[r] = step4_last_nib2(x[r], r, par);
+#else
                 x[r] = r < 3 ? step4_last_shifted(x[r], kShift[r]) : step4_next(x[r], 0u, c);
+#endif
             }
         }
     }
@@ -1013,8 +1032,8 @@ __global__ void k_count(SpanArgs a, uint64_t *nunit, uint4 *irec, uint8_t *fast)
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     __shared__ __attribute__((aligned(16))) uint32_t s8[kTab8Dwords];
     const Tab8 t8 = load_tab8(s8, a.tab8);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
-         i += (uint64_t)gridDim.x * blockDim.x)
+    const uint64_t n = span_count(a);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         count_item<MODE>(a, i, fetch_item<MODE>(a, i), t8, nunit, irec, fast);
 }
 
@@ -1071,9 +1090,10 @@ __device__ __forceinline__ PlanSum plan_at(const uint64_t *nunit, const uint8_t 
 
 // Tile t's sum (thread-contiguous: thread k holds spans t*kPlanTile + 8k .. +7).
 __global__ __launch_bounds__(kPlanThreads) void k_plan_tiles(const uint64_t *nunit, const uint8_t *fast, uint64_t n,
-                                                            PlanSum *tile_sum) {
+                                                            const uint32_t *dn, PlanSum *tile_sum) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     __shared__ PlanSum sh[kPlanThreads / 64];
+    if (dn) n = *dn;
     const uint64_t ntiles = (n + kPlanTile - 1) / kPlanTile;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t i0 = t * kPlanTile + (uint64_t)threadIdx.x * kPlanPer;
@@ -1086,12 +1106,15 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_tiles(const uint64_t *nun
     }
 }
 
-// Exclusive scan of the ntiles tile sums by one workgroup; tile_pre[ntiles] =
-// the grand total (units, blocks and fast spans of the whole batch).
-__global__ __launch_bounds__(kPlanThreads) void k_plan_scan(const PlanSum *tile_sum, uint64_t ntiles,
-                                                           PlanSum *tile_pre) {
+// Exclusive scan of the tile sums of n spans (*dn when given) by one
+// workgroup; *total = the grand total (units, blocks and fast spans of the
+// whole batch).
+__global__ __launch_bounds__(kPlanThreads) void k_plan_scan(const PlanSum *tile_sum, uint64_t n, const uint32_t *dn,
+                                                           PlanSum *tile_pre, PlanSum *total) {
     MCRC_VGPR_FLOOR();
     __shared__ PlanSum sh[kPlanThreads / 64];
+    if (dn) n = *dn;
+    const uint64_t ntiles = (n + kPlanTile - 1) / kPlanTile;
     PlanSum carry{0, 0, 0, 0};
     for (uint64_t t0 = 0; t0 < ntiles; t0 += kPlanThreads) {
         const uint64_t t = t0 + threadIdx.x;
@@ -1100,7 +1123,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_scan(const PlanSum *tile_
         if (t < ntiles) tile_pre[t] = plan_add(carry, ex);
         carry = plan_add(carry, tot);
     }
-    if (threadIdx.x == 0) tile_pre[ntiles] = carry;
+    if (threadIdx.x == 0) *total = carry;
 }
 
 // Exclusive scan of m 32-bit counts by one workgroup (the device page walk:
@@ -1200,14 +1223,16 @@ __device__ __forceinline__ void put_unit(UnitRec *units, const Balance &b, uint6
 // span's units (p0), first block (b0) and, for a one-block span, its slot in
 // the compacted list fastidx (k_blocks).
 __global__ __launch_bounds__(kPlanThreads) void k_expand(const uint8_t *base, const uint64_t *nunit, const uint8_t *fast,
-                                                        const PlanSum *tile_pre, const uint4 *irec, uint64_t n,
-                                                        UnitRec *units, uint64_t cap, uint32_t *nvalid, UnitRec *whole,
-                                                        uint32_t *nwhole, uint4 *big, uint32_t *nbig, uint32_t *fastidx,
-                                                        uint32_t groups, uint32_t *starts) {
+                                                        const PlanSum *tile_pre, const PlanSum *total, const uint4 *irec,
+                                                        uint64_t n, const uint32_t *dn, UnitRec *units, uint64_t cap,
+                                                        uint32_t *nvalid, UnitRec *whole, uint32_t *nwhole, uint4 *big,
+                                                        uint32_t *nbig, uint32_t *fastidx, uint32_t groups,
+                                                        uint32_t *starts) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     __shared__ PlanSum sh[kPlanThreads / 64];
+    if (dn) n = *dn;
     const uint64_t ntiles = (n + kPlanTile - 1) / kPlanTile;
-    const Balance bal = balance_of(tile_pre + ntiles, n, groups, starts);
+    const Balance bal = balance_of(total, n, groups, starts);
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t i0 = t * kPlanTile + (uint64_t)threadIdx.x * kPlanPer;
         uint64_t ck[kPlanPer];
@@ -1254,9 +1279,10 @@ __global__ __launch_bounds__(kPlanThreads) void k_expand(const uint8_t *base, co
 
 // big[b] = {span, p0, b0 (lo, hi)} from k_expand.
 __global__ void k_expand_big(const uint8_t *base, const uint64_t *nunit, const PlanSum *total, const uint4 *irec,
-                             UnitRec *units, const uint4 *big, const uint32_t *nbig, uint64_t n, uint32_t groups,
-                             uint32_t *starts) {
+                             UnitRec *units, const uint4 *big, const uint32_t *nbig, uint64_t n, const uint32_t *dn,
+                             uint32_t groups, uint32_t *starts) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
+    if (dn) n = *dn;
     const Balance bal = balance_of(total, n, groups, starts);
     const uint32_t nb = *nbig;
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
@@ -1306,8 +1332,8 @@ __global__ void k_final(SpanArgs a, const uint4 *irec) {
     Tab8 t8{s8};
     if (!UNITS) t8 = load_tab8(s8, a.tab8);
     uint32_t nb = 0;  // bad spans seen by this thread
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t n = UNITS ? span_count(a) : a.n;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint8_t *p;
         uint32_t len, R, z = 0;
         bool sane;
@@ -1626,6 +1652,7 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
 struct ItemsOut {
     uint32_t *fb;   // items for the planned path (sane, not one block)
     uint32_t *nfb;  // their count
+    const uint32_t *route;  // k_census's verdict (nullptr: take the batch); 0: every image to the planned path
     uint2 *rt;      // MODE 2: per item {M_t(f), t | kRtFused}, {0, 0} if not fused (for k_fix)
 };
 constexpr uint32_t kRtFused = 0x80000000u;
@@ -1681,6 +1708,10 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
     const uint64_t ngroups = (n + 1) / 2;
     const uint64_t grp0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
     if ((uint64_t)blockIdx.x * waves >= ngroups) return;
+    if (MODE != 0 && io.route && *io.route == 0) {  // the census sent the batch to the planned path
+        if (blockIdx.x == 0 && threadIdx.x == 0) *io.nfb = (uint32_t)n;
+        return;
+    }
     load_tables(smem, img, kLdsImageK1Bytes);
     if (grp0 >= ngroups) return;
     const uint32_t lane = threadIdx.x & 63u, li = lane & 31u, g = lane >> 5;
@@ -1905,8 +1936,9 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
 // within k_items an image's stamp could race with another wave's read of the
 // same bytes when images overlap.  (MODE 0 spans get their CRC from the epoch
 // lanes of k_items itself.)
-__global__ void k_fix(SpanArgs a, const uint2 *rt) {
+__global__ void k_fix(SpanArgs a, const uint2 *rt, const uint32_t *route) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
+    if (route && *route == 0) return;  // (k_items took no image)
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint2 r = rt[i];
@@ -1919,16 +1951,49 @@ __global__ void k_fix(SpanArgs a, const uint2 *rt) {
     }
 }
 
-// Fallback lists: gather the listed items' offsets / scatter their results.
-__global__ void k_gather_offs(const uint64_t *offsets, const uint32_t *idx, const uint32_t *nidx, uint64_t *out) {
-    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
-    const uint32_t nn = *nidx;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) out[i] = offsets[idx[i]];
+// K5 or the planned path, decided on the device (round 4; it was the host's
+// guess from the batch's average image size, which a mix of short and long
+// images can match): the headers of up to kCensus images spread evenly over
+// the batch, and *route = 1 when at least 15/16 of them have K5's shape (one
+// 4 KiB block after a short head fragment).  Below that the images K5 leaves
+// to its fallback cost a second pass, and the planned path takes the batch
+// (k_items then lists every image).  One workgroup, one header per thread.
+constexpr uint32_t kCensus = 1024;
+template <int MODE>
+__global__ __launch_bounds__(kCensus) void k_census(SpanArgs a, uint32_t *route) {
+    MCRC_VGPR_FLOOR();
+    __shared__ uint32_t cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    const uint64_t n = a.n, s = min(n, (uint64_t)kCensus);
+    if (threadIdx.x < s) {
+        const uint64_t i = threadIdx.x * n / s;
+        const ItemDesc it = fetch_item<MODE>(a, i);
+        const uint32_t t = tail_pad(it.p, it.len);
+        if (it.sane && fused_vlen(it.len + t)) atomicAdd(&cnt, 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *route = 16ull * cnt >= 15ull * s ? 1u : 0u;
 }
-__global__ void k_scatter_ok(const uint8_t *ok_in, const uint32_t *idx, const uint32_t *nidx, uint8_t *ok) {
+
+// Fallback lists: gather the listed items' offsets / scatter their results.
+// (route 0, k_census: k_items took no image, the list is every image: the
+// identity)
+__global__ void k_gather_offs(const uint64_t *offsets, const uint32_t *idx, const uint32_t *nidx, uint64_t *out,
+                              const uint32_t *route) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     const uint32_t nn = *nidx;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) ok[idx[i]] = ok_in[i];
+    const bool all = route && *route == 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x)
+        out[i] = offsets[all ? i : idx[i]];
+}
+__global__ void k_scatter_ok(const uint8_t *ok_in, const uint32_t *idx, const uint32_t *nidx, uint8_t *ok,
+                             const uint32_t *route) {
+    MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
+    const uint32_t nn = *nidx;
+    const bool all = route && *route == 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x)
+        ok[all ? i : idx[i]] = ok_in[i];
 }
 
 // Chained CRC over an iov list (the chunked-item read verify of

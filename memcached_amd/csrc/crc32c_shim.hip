@@ -84,7 +84,8 @@ struct Device {
     // images): zero between calls, kept so by the kernel's last workgroup
     unsigned long long *small_nbad = nullptr;
     uint32_t *small_done = nullptr;
-    uint32_t *nfb = nullptr, *hfb = nullptr;  // k_items' fallback count (device, pinned twin)
+    uint32_t *nfb = nullptr;    // k_items' fallback count (device)
+    uint32_t *route = nullptr;  // k_census's verdict: K5 (1) or the planned path (0)
     hipStream_t stream = nullptr, copy = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};  // host-batch pipeline slots
@@ -256,8 +257,8 @@ int init_device(Device &d, int id) {
     HIP_OK(hipMalloc(&d.small_nbad, 16));
     HIP_OK(hipMemset(d.small_nbad, 0, 16));
     d.small_done = reinterpret_cast<uint32_t *>(d.small_nbad + 1);
-    HIP_OK(hipMalloc(&d.nfb, sizeof(uint32_t)));
-    HIP_OK(hipHostMalloc(&d.hfb, sizeof(uint32_t), hipHostMallocDefault));
+    HIP_OK(hipMalloc(&d.nfb, 2 * sizeof(uint32_t)));
+    d.route = d.nfb + 1;
     HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
     HIP_OK(hipEventCreate(&d.ev0));
@@ -389,14 +390,10 @@ bool fused_len(uint32_t len) {
     return true;
 }
 
-// Item images whose average size is that of a fused span's image (ntotal
-// 4132..4256 B: 4 KiB values, configs 1 and 5) go through K5; other mixes
-// through the planned path (K5 would send most of them to its fallback).
-bool items_fused(const mcrc_dev::SpanArgs &a) {
-    if (a.n < 4096) return false;
-    const uint64_t avg = a.base_bytes / a.n;
-    return avg >= mcrc_dev::kBlockBytes + 36 && avg <= mcrc_dev::kBlockBytes + 32 + mcrc_dev::kFragMax + 32;
-}
+// Large item batches go through launch_items, where k_census samples their
+// headers on the device and routes them to K5 (one-block images: 4 KiB
+// values, configs 1 and 5) or to the planned path.
+bool items_fused(const mcrc_dev::SpanArgs &a) { return a.n >= 4096; }
 
 // Batches of at most g_small_max spans take the single-launch k_small
 // (crc32c_set_small_max changes it; the parity tests run every case through
@@ -516,20 +513,21 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     // workgroup over them, then each tile rescanned where k_expand uses it
     const uint64_t ntiles = (n + mcrc_dev::kPlanTile - 1) / mcrc_dev::kPlanTile;
     const int gt = (int)std::min<uint64_t>(ntiles, 4096);
+    // (a.dn: n is the list's upper bound and its length is read on the device)
     hipLaunchKernelGGL(mcrc_dev::k_plan_tiles, dim3(gt), dim3(mcrc_dev::kPlanThreads), 0, st,
-                       (const uint64_t *)d.nunit, (const uint8_t *)d.fast, n, d.tile_sum);
+                       (const uint64_t *)d.nunit, (const uint8_t *)d.fast, n, a.dn, d.tile_sum);
+    mcrc_dev::PlanSum *total = d.tile_pre + ntiles;
     hipLaunchKernelGGL(mcrc_dev::k_plan_scan, dim3(1), dim3(mcrc_dev::kPlanThreads), 0, st,
-                       (const mcrc_dev::PlanSum *)d.tile_sum, ntiles, d.tile_pre);
-    const mcrc_dev::PlanSum *total = d.tile_pre + ntiles;
-    const uint32_t *nfast = &d.tile_pre[ntiles].fast;
+                       (const mcrc_dev::PlanSum *)d.tile_sum, n, a.dn, d.tile_pre, total);
+    const uint32_t *nfast = &total->fast;
     uint32_t *const starts = kSpanBalance ? d.starts : nullptr;
     hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(gt), dim3(mcrc_dev::kPlanThreads), 0, st, a.base,
                        (const uint64_t *)d.nunit, (const uint8_t *)d.fast, (const mcrc_dev::PlanSum *)d.tile_pre,
-                       (const uint4 *)d.irec, n, d.units, cap, nvalid, d.whole, nwhole, d.big, nbig, d.fastidx,
-                       span_groups(d), starts);
+                       (const mcrc_dev::PlanSum *)total, (const uint4 *)d.irec, n, a.dn, d.units, cap, nvalid, d.whole,
+                       nwhole, d.big, nbig, d.fastidx, span_groups(d), starts);
     hipLaunchKernelGGL(mcrc_dev::k_expand_big, dim3(1024), dim3(256), 0, st, a.base, (const uint64_t *)d.nunit,
-                       total, (const uint4 *)d.irec, d.units, (const uint4 *)d.big, (const uint32_t *)nbig, n,
-                       span_groups(d), starts);
+                       (const mcrc_dev::PlanSum *)total, (const uint4 *)d.irec, d.units, (const uint4 *)d.big,
+                       (const uint32_t *)nbig, n, a.dn, span_groups(d), starts);
     mcrc_dev::SpanArgs u = a;
     u.units = d.units;
     u.nunits = nvalid;
@@ -552,9 +550,10 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
 }
 
 // K5 over the item images of a (MODE 1 verify, MODE 2 stamp; device memory,
-// a.nbad zeroed by the caller): k_items (+ k_fix for stamps), then the
-// planned path over the images it listed as not one block.  Synchronous: the
-// length of that list is read back.
+// a.nbad zeroed by the caller): k_census routes the batch on the device,
+// k_items checksums the one-block images (+ k_fix for stamps) and lists the
+// others, and the planned path takes that list with its length read on the
+// device (a.dn).  Nothing is read back: an async stamp stays async.
 template <int MODE>
 int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     const uint64_t n = a.n;
@@ -562,37 +561,32 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     mcrc_dev::ItemsOut io{};
     io.fb = (uint32_t *)d.grow(kScrFb, n * 4);
     io.nfb = d.nfb;
+    io.route = d.route;
     if (MODE == 2) io.rt = (uint2 *)d.grow(kScrRt, n * 8);
-    if (!io.fb || (MODE == 2 && !io.rt)) return CRC32C_ENOMEM;
+    uint64_t *fo = (uint64_t *)d.grow(kScrFbOffs, n * 8);
+    uint8_t *fok = (uint8_t *)d.grow(kScrFbOk, n);
+    if (!io.fb || (MODE == 2 && !io.rt) || !fo || !fok) return CRC32C_ENOMEM;
     HIP_OK(hipMemsetAsync(d.nfb, 0, 4, st));
+    hipLaunchKernelGGL(mcrc_dev::k_census<MODE>, dim3(1), dim3(mcrc_dev::kCensus), 0, st, a, d.route);
     hipLaunchKernelGGL((mcrc_dev::k_items<MODE, true>), dim3(grid_for(d, n)), dim3(1024),
                        mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
+    const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 1024);
     if (MODE == 2)
-        hipLaunchKernelGGL(mcrc_dev::k_fix, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 1024)), dim3(256),
-                           0, st, a, (const uint2 *)io.rt);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(d.hfb, d.nfb, 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    const uint64_t nfb = *d.hfb;
-    if (nfb == 0) return CRC32C_OK;
-    uint64_t *fo = (uint64_t *)d.grow(kScrFbOffs, nfb * 8);
-    uint8_t *fok = (uint8_t *)d.grow(kScrFbOk, nfb);
-    if (!fo || !fok) return CRC32C_ENOMEM;
-    const unsigned g = (unsigned)std::min<uint64_t>((nfb + 255) / 256, 1024);
+        hipLaunchKernelGGL(mcrc_dev::k_fix, dim3(g), dim3(256), 0, st, a, (const uint2 *)io.rt,
+                           (const uint32_t *)d.route);
     hipLaunchKernelGGL(mcrc_dev::k_gather_offs, dim3(g), dim3(256), 0, st, a.offsets, (const uint32_t *)io.fb,
-                       (const uint32_t *)d.nfb, fo);
+                       (const uint32_t *)d.nfb, fo, (const uint32_t *)d.route);
+    HIP_OK(hipGetLastError());
     mcrc_dev::SpanArgs f = a;
     const bool want_ok = MODE == 1 || a.ok;
     f.offsets = fo;
-    f.n = nfb;
+    f.dn = d.nfb;  // (f.n = n: the list's upper bound)
     f.ok = want_ok ? fok : nullptr;
-    Path path;
-    path.small = takes_small<MODE>(f);
-    int rc = launch_units<MODE>(d, f, st, path);
+    int rc = launch_units<MODE>(d, f, st, Path{});
     if (rc) return rc;
     if (want_ok)
         hipLaunchKernelGGL(mcrc_dev::k_scatter_ok, dim3(g), dim3(256), 0, st, (const uint8_t *)fok,
-                           (const uint32_t *)io.fb, (const uint32_t *)d.nfb, a.ok);
+                           (const uint32_t *)io.fb, (const uint32_t *)d.nfb, a.ok, (const uint32_t *)d.route);
     HIP_OK(hipGetLastError());
     return CRC32C_OK;
 }
@@ -956,9 +950,8 @@ int item_images(void *base, uint64_t base_bytes, uint64_t region_bytes, const ui
         a.ok = ok;
         a.out = nullptr;  // stamp: write into the images
         path.host_counted = path.small;
-        // K5 for synchronous calls over one-block images (it reads back the
-        // length of its fallback list)
-        const bool k5 = !path.small && !((flags & CRC32C_ASYNC) && !nbad) && items_fused(a);
+        // large batches: K5 or the planned path, routed on the device
+        const bool k5 = !path.small && items_fused(a);
         d->acquire(st);
         if (!path.host_counted) (void)hipMemsetAsync(d->nbad, 0, sizeof(unsigned long long), st);
         rc = k5 ? launch_items<MODE>(*d, a, st) : launch_units<MODE>(*d, a, st, path);

@@ -541,3 +541,85 @@ def test_partly_registered_buffer_is_staged_not_read_in_place(torch):
         assert nbad == 0 and ok.all()
     finally:
         _lib.check(_lib.lib.crc32c_host_unregister(ctypes.c_void_p(arena.ctypes.data)), "unregister")
+
+
+@pytest.mark.parametrize("mix", ["fused", "mixed41"])
+def test_k5_census_routes_by_shape(torch, mix):
+    """Large item batches are routed on the device (k_census): all 4 KiB
+    values (the K5 shape) and a mix of 2 KiB and 6.2 KiB values whose average
+    image is also ~4.1 KiB (the old host rule's guess sent it to K5).  Verify
+    and stamp are exact either way, including a damaged image per 97."""
+    rng = np.random.default_rng(91 if mix == "fused" else 92)
+    wbuf = 1 << 20
+    n = 5000
+    vals = [4096] * n if mix == "fused" else [2048 if i % 2 else 6150 for i in range(n)]
+    items = [layout.make_item(b"key%07d" % i, rng.integers(0, 256, v, dtype=np.uint8).tobytes(), cas=i + 1)
+             for i, v in enumerate(vals)]
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    if mix == "mixed41":
+        assert 4100 <= buf.size / n <= 4300
+    soffs, slens = layout.spans_of(buf, offs)
+    crcs = oracle.batch(buf, soffs, slens)
+    layout.store_crcs(buf, offs, crcs)
+    victims = np.arange(5, n, 97)
+    for v in victims.tolist():
+        buf[int(soffs[v]) + 100] ^= 2
+    d = torch.from_numpy(buf).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    ok, nbad = mc.verify_items(d, do, region_bytes=wbuf)
+    assert nbad == victims.size
+    np.testing.assert_array_equal(np.flatnonzero(ok.cpu().numpy() == 0), victims)
+    # stamp with exptime zeroed: every image gets the oracle's spill CRC
+    z = buf.copy()
+    layout.store_crcs(z, offs, np.zeros(n, np.uint32))
+    dz = torch.from_numpy(z).cuda()
+    ok, nbad = mc.stamp_items(dz, do, region_bytes=wbuf)
+    assert nbad == 0 and bool(ok.all())
+    np.testing.assert_array_equal(_stored(dz.cpu().numpy(), offs), oracle.batch(z, soffs, slens))
+
+
+def test_async_device_stamp_returns_before_the_kernels_finish(torch):
+    """crc32c_stamp_items with CRC32C_DEVICE | CRC32C_ASYNC and nbad == NULL
+    over a K5-sized batch enqueues everything (census, k_items, k_fix and the
+    planned fallback with a device-side count) and returns: no read-back in
+    the middle.  Queued behind several milliseconds of K1 work, the stream is
+    still busy when the call returns; after a sync every stamp is exact."""
+    n, nt = 20000, 4165
+    g = torch.Generator(device="cuda").manual_seed(12)
+    d = torch.randint(0, 256, (n * nt + 64,), dtype=torch.uint8, device="cuda", generator=g)
+    im = d[:n * nt].view(n, nt)
+    im[:, 28:32] = 0
+    im[:, 32:36] = torch.tensor([4098 & 255, 4098 >> 8, 0, 0], dtype=torch.uint8, device="cuda")
+    im[:, 38:40] = torch.tensor([2, 0], dtype=torch.uint8, device="cuda")
+    im[:, 41] = 10
+    im[::7, 32:36] = torch.tensor([0, 8, 0, 0], dtype=torch.uint8, device="cuda")  # nbytes 2048: not one block
+    offs = np.arange(n, dtype=np.uint64) * nt
+    doffs = torch.from_numpy(offs.view(np.int64)).cuda()
+    host = d.cpu().numpy()
+    soffs, slens = layout.spans_of(host, offs)
+    want = oracle.batch(host, soffs, slens)
+    def stamp():
+        return _lib.lib.crc32c_stamp_items(ctypes.c_void_p(d.data_ptr()), ctypes.c_uint64(d.numel()),
+                                           ctypes.c_uint64(0), ctypes.c_void_p(doffs.data_ptr()), ctypes.c_uint64(n),
+                                           None, None, _lib.CRC32C_DEVICE | _lib.CRC32C_ASYNC,
+                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    # (a first call grows the library's scratch -- hipFree synchronises the
+    # device -- and must stamp the same)
+    _lib.check(stamp(), "async stamp")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_stored(d.cpu().numpy(), offs), want)
+    im[:, 28:32] = 0
+    big = torch.randint(0, 256, (1 << 30,), dtype=torch.uint8, device="cuda", generator=g)
+    kout = torch.empty(1 << 18, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    for _ in range(16):  # ~3 ms of K1 ahead of the stamp on the same stream
+        _lib.check(_lib.lib.crc32c_batch(ctypes.byref(_lib.Spans(big.data_ptr(), big.numel(), None, 4096, None,
+                                                                 4096, None, kout.data_ptr(), 1 << 18)),
+                                         _lib.CRC32C_DEVICE | _lib.CRC32C_ASYNC, ctypes.c_void_p(st.cuda_stream)))
+    rc = stamp()
+    busy = not st.query()
+    _lib.check(rc, "async stamp")
+    torch.cuda.synchronize()
+    assert busy, "the async stamp waited for the stream"
+    np.testing.assert_array_equal(_stored(d.cpu().numpy(), offs), want)
