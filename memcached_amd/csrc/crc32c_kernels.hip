@@ -98,6 +98,25 @@ __device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &
             }
         }
     }
+#if defined(MCRC_K1_SENS)
+    // sensitivity ablations (timing only): 1 = +64 VALU per lane-step
+    // (dependent v_xor), 2 = +32 conflict-free LDS reads (+16 v_bitop3)
+    uint32_t z = x[0];
+    if constexpr (MCRC_K1_SENS == 1) {
+#pragma unroll
+        for (int k = 0; k < 64; ++k) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z) : "v"(x[k & 3]));
+    } else {
+#pragma unroll
+        for (int k = 0; k < 32; k += 2) {
+            const uint32_t a = lds_ld(kAux4Bytes + 256u * (uint32_t)k + c.lane4);
+            const uint32_t b = lds_ld(kAux4Bytes + 256u * (uint32_t)k + 256u + c.lane4);
+            z = xor3(z, a, b);
+        }
+        asm volatile("" : "+v"(z));
+    }
+    x[0] ^= z & 0u;
+    asm volatile("" :: "v"(z));
+#endif
     return xor3(x[0], x[1], x[2]) ^ x[3];
 }
 
@@ -1781,6 +1800,9 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
     auto prep_pieces = [&]() {
 #pragma unroll
         for (uint32_t k = 0; k < kFragPieces; ++k) pc[k] = ld16(k < p_np16 ? gb + p_pho + 16 * k : gz);
+#if defined(MCRC_K5_ABL) && (MCRC_K5_ABL & 1)  // ablation: no fragment reads (results wrong)
+        for (uint32_t k = 0; k < kFragPieces; ++k) pc[k] = ld16(gz);
+#endif
     };
     // r = register from ~c over [p, G): the pieces of [floor16(p), G), bytes
     // below p cleared and ~c injected at p (head_dword); C = M_4096(r)
@@ -1805,10 +1827,24 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
     // Loads of step s (< ns, else a repeat of the epoch's last step, whose
     // result is not used) into b: its block and its status.
     auto ld = [&](ItemBuf &b, uint32_t s, uint32_t ns) {
+#if defined(MCRC_K5_RL)
+        // (the step is wave-uniform: the two groups' descriptors are lanes
+        // 2s and 2s + 1, read as scalars, no ds_bpermute)
+        const int s2 = (int)__builtin_amdgcn_readfirstlane(2 * min(s, ns - 1));
+        const uint32_t lo0 = __builtin_amdgcn_readlane(eglo, s2), lo1 = __builtin_amdgcn_readlane(eglo, s2 + 1);
+        const uint32_t hi0 = __builtin_amdgcn_readlane(eghi, s2), hi1 = __builtin_amdgcn_readlane(eghi, s2 + 1);
+        const uint32_t st0 = __builtin_amdgcn_readlane(est, s2), st1 = __builtin_amdgcn_readlane(est, s2 + 1);
+        const uint64_t lo = g ? lo1 : lo0, hi = g ? hi1 : hi0;
+        b.st = g ? st1 : st0;
+#else
         const int src = (int)(2 * min(s, ns - 1) + g);
         const uint64_t lo = (uint32_t)__shfl((int)eglo, src, 64), hi = (uint32_t)__shfl((int)eghi, src, 64);
         b.st = (uint32_t)__shfl((int)est, src, 64);
+#endif
         gbyte *blk = (b.st & kStFused) ? gb + (lo | (hi << 32)) : gz;
+#if defined(MCRC_K5_ABL) && (MCRC_K5_ABL & 2)  // ablation: blocks on 128-B lines (results wrong)
+        blk = (gbyte *)((uintptr_t)blk & ~(uintptr_t)127);
+#endif
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll

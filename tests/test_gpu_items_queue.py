@@ -253,6 +253,43 @@ def test_batch_multi_matches_oracle(torch):
     np.testing.assert_array_equal(mc.shard_cuts(lens, 8), shard.plan(lens, 8))
 
 
+def test_batch_multi_config4_shape_every_device(torch):
+    """BASELINE config 4's shape (equal 4 KiB items at stride 4096, one pinned
+    host batch) split by crc32c_batch_multi over every visible device
+    (torch.cuda.device_count(): the device != 0 paths run wherever the box has
+    more than one), and over each device alone; every CRC against the oracle."""
+    ng = torch.cuda.device_count()
+    n = 32768 * max(ng, 2)
+    host = torch.randint(0, 256, (n * 4096,), dtype=torch.uint8).pin_memory()
+    buf = host.numpy()
+    want = oracle.batch(buf, np.arange(n, dtype=np.uint64) * 4096, np.full(n, 4096, np.uint64))
+    out = np.empty(n, np.uint32)
+    sp = _lib.Spans(host.data_ptr(), host.numel(), None, 4096, None, 4096, None, out.ctypes.data, n)
+    _lib.check(_lib.lib.crc32c_batch_multi(ctypes.byref(sp), ng), "batch_multi")
+    np.testing.assert_array_equal(out, want)
+    cuts = mc.shard_cuts(np.full(n, 4096, np.uint32), ng)
+    assert cuts[0] == 0 and cuts[-1] == n and all(int(cuts[g + 1] - cuts[g]) == n // ng for g in range(ng))
+    for g in range(ng):  # each device alone, as the current device
+        with torch.cuda.device(g):
+            out[:] = 0
+            _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp), 0, None), f"device {g}")
+            np.testing.assert_array_equal(out, want)
+
+
+def test_bench_headline_over_every_device_in_one_process(torch):
+    """bench.py --gpus N without a launcher (the driver's way of starting it):
+    headline_devices runs K1 on every visible device from one process and
+    prints the bench line with n_gpus = N (small batches here)."""
+    import argparse
+    import bench
+    ng = torch.cuda.device_count()
+    args = argparse.Namespace(gpus=ng, steps=3, warmup=1, settle_ms=0.0, items=1 << 14, fill="splitmix",
+                              no_cpu_baseline=True, events="region")
+    res = bench.headline_devices(args)
+    assert res["n_gpus"] == ng and res["value"] > 0 and len(res["kernel_ms_per_device"]) == ng
+    assert res["roofline"]["frac"] > 0 and res["scaling"] == "weak"
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -266,7 +303,7 @@ def _rank_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from memcached_amd import crc32c as mcl
     from memcached_amd import shard as sh
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(rank % torch.cuda.device_count())  # (one device per rank where there are several)
     rng = np.random.default_rng(77)  # the same batch on every rank
     lens = np.minimum(rng.zipf(1.2, 5000) * 32, 1 << 20).astype(np.uint32)
     offs = np.concatenate([[1], 1 + np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
