@@ -93,6 +93,11 @@ constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 #ifndef MCRC_NIB
 #define MCRC_NIB 0
 #endif
+// MCRC_K5_ITEMS=1: K5 as k_items (round 3, 16-B-anchored blocks) instead of
+// the line-anchored k_lines (A/B builds)
+#ifndef MCRC_K5_ITEMS
+#define MCRC_K5_ITEMS 0
+#endif
 // Nibble form of the shifted tables (MCRC_NIB): set s (row chain s, shift
 // M_{(3-s)*1024}) holds 8 tables of 16 entries, table 2k + h for nibble h of
 // byte k, at kNibShiftBytes + 512 s + 64 (2k + h).  A 16-entry table spans 16

@@ -169,8 +169,13 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     auto ld = [&](Regs &r, uint64_t gi) {
         const uint64_t gu = gi < ngroups ? gi : gi - gstep < ngroups ? gi - gstep : ngroups - 1;
         const uint64_t first = gu * IPW;
-        const uint8_t *wb = base + first * stride;
-        const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
+        // (round 4) the prefetch past the wave's last group reads the table
+        // image (L2-resident: every workgroup copied it) instead of repeating
+        // that group: the repeat came a whole step later, out of L2 again,
+        // and cost 1/128 of the launch's HBM reads
+        const bool past = gi >= ngroups;
+        const uint8_t *wb = past ? reinterpret_cast<const uint8_t *>(img) : base + first * stride;
+        const uint32_t gl = past ? 0u : first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
         // crc_in first: it is consumed before the first chain step, and
         // vmcnt counts in issue order (issued last, it made the step wait for
         // all of its loads before any chain could start)
@@ -1673,6 +1678,8 @@ struct ItemsOut {
     uint32_t *nfb;  // their count
     const uint32_t *route;  // k_census's verdict (nullptr: take the batch); 0: every image to the planned path
     uint2 *rt;      // MODE 2: per item {M_t(f), t | kRtFused}, {0, 0} if not fused (for k_fix)
+    const uint32_t *xk;  // k_lines: x^(8e) for e in [kXkLo, kXkLo + kXkN)
+    uint32_t nsr;        // k_lines: steps per run (a wave's run is 2 nsr consecutive images)
 };
 constexpr uint32_t kRtFused = 0x80000000u;
 
@@ -1966,6 +1973,297 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
     if (lane == 0 && nb) atomicAdd(a.nbad, (unsigned long long)nb);
 }
 
+// ===========================================================================
+// K5, line-anchored (k_lines, round 4)
+// ===========================================================================
+//
+// k_items reads each image's header and head fragment at the start of an
+// epoch and the image's 16-B-anchored block up to 32 steps later, by when the
+// lines they share (the block's first line, the previous block's last line,
+// which holds this image's header) have left L2: config 5 fetched 1.08x its
+// span bytes, config 2r 1.065x (profiles/r04_ablations).  Here no line is
+// read by both a block and a per-lane prep:
+//   - the block of span D = [p, E) is the window [A, A + 4096), A =
+//     ceil128(p + 4): the whole lines [A, B) of D, B = floor128(E), and zeros
+//     past B (31 or 32 lines: the fused shape; lanes 28-31 of row 3 read the
+//     zero line for a 31-line window);
+//   - the epoch lane of the image takes its head [p, A) (4..131 bytes, ~c
+//     injected at p: r_h = register from ~c over [p, A)) and its tail
+//     [B, Et), Et = ceil16(E), bytes from E on cleared (r_t);
+//   - a wave's epoch is a run of 2 nsr CONSECUTIVE images (lane L prepares
+//     image L of the run, step s checksums images 2s and 2s + 1), so one
+//     image's tail and the next image's head and header -- the same one or
+//     two lines -- are read by neighbouring lanes of one instruction;
+//   - the group's R = raw of the window goes back to the image's epoch lane,
+//     which at the end of the run forms
+//       V = M_{Et-A}(r_h) ^ M_{Et-A-4096}(R) ^ r_t = M_pad(f),
+//     f the register after D from ~c, pad = Et - E (x^(8e) from the xk table,
+//     e in [-128, 4352)): crc32c(c, D) = ~M_{-pad}(V); a verify is good iff
+//     V == M_pad(~stored).
+// tests/test_items_lines_model.py restates it on the CPU.
+constexpr uint32_t kLineBytes = 128;
+constexpr uint32_t kHeadPieces = 10;  // 16-B pieces of [floor16(p), A): A - p <= 131
+constexpr uint32_t kTailPieces = 9;   // of [B, Et): Et - B < 128 + 16
+constexpr int32_t kXkLo = -128;
+constexpr uint32_t kXkN = 4480;       // e in [-128, 4352)
+constexpr uint32_t kSt31 = 0x80u;     // the window holds 31 lines (row 3, lanes 28-31: zeros)
+
+// The fused shape: B - A (bytes of whole lines inside the span after the
+// head) is 31 or 32 lines.
+__host__ __device__ __forceinline__ bool lines_fused(int64_t lines_bytes) {
+    return lines_bytes >= (int64_t)(kBlockBytes - kLineBytes) && lines_bytes <= (int64_t)kBlockBytes;
+}
+
+template <int MODE, bool OFFS>
+__global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restrict__ img, ItemsOut io) {
+    // MODE 0: equal spans of a.len bytes by offsets (OFFS) or stride, MODE 1/2:
+    // item images (verify / stamp) by offsets
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint64_t n = a.n;
+    const uint32_t nsr = io.nsr;
+    const uint64_t run_imgs = 2ull * nsr;
+    const uint64_t nruns = (n + run_imgs - 1) / run_imgs;
+    const uint64_t waves = blockDim.x >> 6;
+    const uint64_t W = gridDim.x * waves;
+    const uint64_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
+    if ((uint64_t)blockIdx.x * waves >= nruns) return;
+    if (MODE != 0 && io.route && *io.route == 0) {  // the census sent the batch to the planned path
+        if (blockIdx.x == 0 && threadIdx.x == 0) *io.nfb = (uint32_t)n;
+        return;
+    }
+    load_tables(smem, img, kLdsImageK1Bytes);
+    if (w0 >= nruns) return;
+    const uint32_t lane = threadIdx.x & 63u, li = lane & 31u, g = lane >> 5;
+    LaneCtx c;
+    c.lane4 = li << 2;
+    c.lane4hi = c.lane4 | 0x10000u;
+    gbyte *const gb = (gbyte *)a.base;
+    gbyte *const gz = (gbyte *)(a.zero + (blockIdx.x % kZeroSlots) * (4096 / 16));
+    const uint32_t base_lo = (uint32_t)(uintptr_t)a.base;  // (alignments: the offsets are from a.base)
+    uint32_t nb = 0;  // bad (malformed or mismatching) images seen by this lane
+
+    auto item_of = [&](uint64_t r) -> uint64_t { return r * run_imgs + lane; };
+    auto valid_of = [&](uint64_t r) { return lane < run_imgs && r < nruns && item_of(r) < n; };
+    auto off_of = [&](uint64_t r) -> uint64_t {
+        // (offsets or stride is a template choice: a load on one side of a
+        // branch leaves the waitcnt pass a merged state that waits for it)
+        return valid_of(r) ? (OFFS ? a.offsets[item_of(r)] : item_of(r) * a.stride) : 0;
+    };
+    // MODE 0: x^(-8t), t < 16, lane-distributed (lane j holds t = j & 15)
+    const uint32_t xinv = MODE == 0 ? a.xpow[kXpowInv + (lane & 15u)] : 0u;
+    uint64_t noff = off_of(w0);  // this lane's image offset in the wave's next run
+    uint32_t ncin = MODE == 0 && a.crc_in && valid_of(w0) ? a.crc_in[item_of(w0)] : 0u;
+
+    // this lane's image of the run
+    uint32_t eglo = 0, eghi = 0, est = 0;  // window start A (offset from a.base), status
+    uint32_t p_kh = 0, p_inj = ~0u, p_stored = 0, p_nh = 0, p_nt = 0, p_eta = 0;
+    uint64_t p_pho = 0, p_b = 0;
+    uint32_t r_h = 0, r_t = 0, er = 0;
+    uint4 pc[kHeadPieces];
+    auto prep_head = [&](uint64_t r) {
+        const bool valid = valid_of(r);
+        const uint64_t off = noff;
+        ItemHdr h{0u, 0u, 0u, 0u};
+        ItemDesc it{a.base, 0u, 0u, false};
+        p_inj = ~0u;  // ~c: the register's initial value, XORed in at p
+        if (MODE == 0) {
+            it.sane = valid && off <= a.base_bytes && a.len <= a.base_bytes - off;
+            it.len = a.len;
+            if (a.crc_in) p_inj = ~ncin;
+        } else {
+            const bool hdr_ok = valid && off + 48 <= a.base_bytes;
+            if (hdr_ok) h = parse_hdr(gb + off);
+            it = item_desc(a, off, h, hdr_ok);
+        }
+        p_stored = h.exptime;
+        const uint32_t len = it.sane ? it.len : 0u;
+        const uint64_t po = MODE == 0 ? off : off + 32;  // span start (offset)
+        const uint64_t pe = po + len;                     // span end
+        const uint32_t pa = base_lo + (uint32_t)po, ea = base_lo + (uint32_t)pe;
+        const uint64_t A = po + 4 + ((0u - (pa + 4u)) & (kLineBytes - 1));
+        const uint64_t B = pe - (ea & (kLineBytes - 1));
+        const uint32_t pad = (0u - ea) & (kTailAlign - 1);
+        const bool fused = it.sane && len >= 4 && lines_fused((int64_t)B - (int64_t)A);
+        p_kh = pa & 15u;
+        p_pho = po - p_kh;
+        p_b = B;
+        p_nh = fused ? (uint32_t)(A - p_pho) >> 4 : 0u;
+        p_nt = fused ? (uint32_t)(pe + pad - B) >> 4 : 0u;
+        p_eta = (uint32_t)(pe + pad - A);  // Et - A
+        eglo = (uint32_t)A;
+        eghi = (uint32_t)(A >> 32);
+        est = pad | (fused ? kStFused : 0u) | (it.sane ? kStSane : 0u) | (valid ? kStValid : 0u) |
+              (fused && B - A < kBlockBytes ? kSt31 : 0u);
+    };
+    auto head_loads = [&]() {
+#pragma unroll
+        for (uint32_t k = 0; k < kHeadPieces; ++k) pc[k] = ld16(k < p_nh ? gb + p_pho + 16 * k : gz);
+    };
+    // r_h = register from ~c over [p, A): bytes below p cleared, ~c injected at p
+    auto head_chain = [&]() {
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kHeadPieces; ++k) {
+            const uint32_t w[4] = {pc[k].x, pc[k].y, pc[k].z, pc[k].w};
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const int32_t pa = (int32_t)p_kh - (int32_t)(16 * k + 4 * j);
+                const uint32_t d = head_dword(w[j], pa, p_inj);
+                const uint32_t nx = (k == 0 && j == 0) ? d : step4_next(x, d, c);
+                x = k < p_nh ? nx : x;
+            }
+        }
+        r_h = p_nh ? step4_next(x, 0u, c) : 0u;
+    };
+    // (the last piece's bytes from E on are cleared: pad of them)
+    auto tail_loads = [&]() {
+#pragma unroll
+        for (uint32_t k = 0; k < kTailPieces; ++k) {
+            pc[k] = ld16(k < p_nt ? gb + p_b + 16 * k : gz);
+        }
+    };
+    auto tail_chain = [&]() {
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kTailPieces; ++k) {
+            const uint4 v = k + 1 == p_nt ? clear_high(pc[k], est & 15u) : pc[k];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t nx = (k == 0 && j == 0) ? w[j] : step4_next(x, w[j], c);
+                x = k < p_nt ? nx : x;
+            }
+        }
+        r_t = p_nt ? step4_next(x, 0u, c) : 0u;
+    };
+    // Loads of step s (< ns, else a repeat of the run's last step, whose
+    // result is not used) into b: its window and its status.
+    auto ld = [&](ItemBuf &b, uint32_t s, uint32_t ns) {
+        const int src = (int)(2 * min(s, ns - 1) + g);
+        const uint64_t lo = (uint32_t)__shfl((int)eglo, src, 64), hi = (uint32_t)__shfl((int)eghi, src, 64);
+        b.st = (uint32_t)__shfl((int)est, src, 64);
+        // (a step past the run -- the prefetch after its last step -- reads
+        // the workgroup's zero line: a repeat of the last step came a step
+        // later, out of L2 again, and cost 1/32 of the run's HBM reads)
+        gbyte *blk = (b.st & kStFused) && s < ns ? gb + (lo | (hi << 32)) : gz;
+        const bool z3 = (b.st & kSt31) && li >= 28u;  // row 3 past B: zeros
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) b.d.d[r][q] = ld16(blk + r * 1024 + li * 32 + 16 * q);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) b.d.d[3][q] = ld16(z3 ? gz + 16 * q : blk + 3072 + li * 32 + 16 * q);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto part0 = [&](ItemBuf &b) { return reduce_level<0>(lane_partial_x3s<32>(b.d, c), (lane & 1u) == 0u); };
+    // The epoch lanes collect R of their images from the lanes that finished
+    // them (steps s0 .. s0 + cnt - 1 in lanes 0 .. cnt - 1 of each group).
+    auto collect = [&](uint32_t r, uint32_t s0, uint32_t cnt) {
+        const uint32_t sl = lane >> 1;
+        const int src = (int)((lane & 1u) * 32u + (sl - s0));
+        const uint32_t v = (uint32_t)__shfl((int)r, sl - s0 < cnt ? src : 0, 64);
+        er = sl - s0 < cnt ? v : er;
+    };
+    // End of a run: every epoch lane finishes its image.
+    auto finish_run = [&](uint64_t r) {
+        const bool valid = valid_of(r);
+        const uint64_t item = item_of(r);
+        const bool fused = est & kStFused, sane = est & kStSane;
+        const uint32_t pad = est & 15u;
+        // (every lane: a lane-distributed value read under a branch would come
+        // from lanes the branch left inactive)
+        const uint32_t xt = MODE == 0 ? (uint32_t)__shfl((int)xinv, (int)pad, 64) : 0u;
+        uint32_t v = 0;
+        if (fused) {
+            const uint32_t x1 = io.xk[p_eta - kXkLo], x2 = io.xk[p_eta - kBlockBytes - kXkLo];
+            v = mulmodp_dev(r_h, x1) ^ mulmodp_dev(er, x2) ^ r_t;  // M_pad(f)
+        }
+        if (valid) {
+            if (MODE == 0) {
+                a.out[item] = fused ? ~mulmodp_dev(v, xt) : 0u;
+                nb += !sane;  // (out of the buffer: not read, out 0, counted)
+            } else if (MODE == 1) {
+                if (fused || !sane) {
+                    const bool good = fused && v == zeros_lds(~p_stored, pad, c);
+                    a.ok[item] = good;
+                    nb += !good;
+                }
+            } else {
+                io.rt[item] = fused ? make_uint2(v, pad | kRtFused) : make_uint2(0u, 0u);
+                if (!sane) {
+                    if (a.ok) a.ok[item] = 0;
+                    ++nb;
+                }
+            }
+        }
+        if (MODE != 0) {
+            const bool fb = valid && sane && !fused;
+            const uint64_t m = __ballot(fb);  // the fallback list: one atomic per wave with entries
+            if (m) {
+                const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+                uint32_t base = 0;
+                if (lane == first) base = atomicAdd(io.nfb, (uint32_t)__popcll(m));
+                base = __shfl(base, (int)first, 64);
+                if (fb) io.fb[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)item;
+            }
+        }
+    };
+    ItemBuf ra, rb;
+    for (uint64_t r = w0; r < nruns; r += W) {
+        const uint64_t left = n - r * run_imgs;
+        const uint32_t ns = (uint32_t)min((uint64_t)nsr, (left + 1) / 2);
+        prep_head(r);
+        head_loads();
+        // the next run's offsets (and initial CRCs), consumed one run later
+        noff = off_of(r + W);
+        if (MODE == 0) ncin = a.crc_in && valid_of(r + W) ? a.crc_in[item_of(r + W)] : 0u;
+        ld(ra, 0, ns);
+        head_chain();
+        tail_loads();
+        tail_chain();
+        er = 0;
+        uint32_t s = 0;
+        for (; s + 4 <= ns; s += 4) {
+            ld(rb, s + 1, ns);
+            const uint32_t va = part0(ra);
+            ld(ra, s + 2, ns);
+            const uint32_t vb = part0(rb);
+            const uint32_t vab = group_pair_level1(va, vb, lane);
+            ld(rb, s + 3, ns);
+            const uint32_t vc = part0(ra);
+            ld(ra, s + 4, ns);
+            const uint32_t vd = part0(rb);
+            collect(group_reduce32_quad_span(vab, group_pair_level1(vc, vd, lane), lane), s, 4);
+        }
+        for (; s + 2 <= ns; s += 2) {
+            ld(rb, s + 1, ns);
+            const uint32_t va = part0(ra);
+            ld(ra, s + 2, ns);
+            const uint32_t vb = part0(rb);
+            collect(group_reduce32_pair_span(va, vb, lane), s, 2);
+        }
+        if (s < ns) {
+            const uint32_t v = part0(ra);
+            // (part0 ran level 0; levels 1..4 of the span tree)
+            uint32_t t = reduce_level<1>(v, (lane & 3u) == 0u);
+            t = reduce_level<2>(t, (lane & 7u) == 0u);
+            t = reduce_level<3>(t, (lane & 15u) == 0u);
+            t = reduce_level4_span(t, (lane & 31u) == 0u);
+            collect(t, s, 1);
+        }
+        finish_run(r);
+    }
+    // one atomic per wave for the bad count
+    nb += __shfl_xor(nb, 1);
+    nb += __shfl_xor(nb, 2);
+    nb += __shfl_xor(nb, 4);
+    nb += __shfl_xor(nb, 8);
+    nb += __shfl_xor(nb, 16);
+    nb += __shfl_xor(nb, 32);
+    if (lane == 0 && nb) atomicAdd(a.nbad, (unsigned long long)nb);
+}
+
+
 // The last step of a K5 stamp (MODE 2), one thread per image: from R = M_t(f),
 // f the register after the span from ~0, the CRC is ~M_{-t}(R), stamped into
 // the image's exptime as the spill CRC (storage.c:567).  A separate pass:
@@ -2005,8 +2303,14 @@ __global__ __launch_bounds__(kCensus) void k_census(SpanArgs a, uint32_t *route)
     if (threadIdx.x < s) {
         const uint64_t i = threadIdx.x * n / s;
         const ItemDesc it = fetch_item<MODE>(a, i);
-        const uint32_t t = tail_pad(it.p, it.len);
-        if (it.sane && fused_vlen(it.len + t)) atomicAdd(&cnt, 1u);
+#if MCRC_K5_ITEMS
+        const bool fused = fused_vlen(it.len + tail_pad(it.p, it.len));
+#else
+        const uint64_t pa = (uintptr_t)it.p, A = (pa + 4 + kLineBytes - 1) & ~(uint64_t)(kLineBytes - 1);
+        const uint64_t B = (pa + it.len) & ~(uint64_t)(kLineBytes - 1);
+        const bool fused = it.len >= 4 && lines_fused((int64_t)B - (int64_t)A);
+#endif
+        if (it.sane && fused) atomicAdd(&cnt, 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) *route = 16ull * cnt >= 15ull * s ? 1u : 0u;

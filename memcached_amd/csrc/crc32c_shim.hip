@@ -77,6 +77,7 @@ struct Device {
     uint32_t *tab8 = nullptr;   // byte-wise table (k_count / k_final: a span's head fragment and foreign bytes)
     uint4 *img_k1 = nullptr;    // K1 image (160 KiB, crc32c_gf2.h build_lds_image_k1)
     uint32_t *xpow = nullptr;   // x^(8n) table (layout mcrc_dev::kXpow*)
+    uint32_t *xk = nullptr;     // k_lines: x^(8e), e in [kXkLo, kXkLo + kXkN)
     uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
     unsigned long long *nbad = nullptr;  // [0]: bad / out-of-range count, [1]: walk invariant failures
     unsigned long long *hbad = nullptr;  // pinned twin of nbad[0..1] (a D2H copy into pageable memory is a slow path)
@@ -250,6 +251,17 @@ int init_device(Device &d, int id) {
     HIP_OK(hipMemcpy(d.segpow, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&d.xpow, xp.size() * 4));
     HIP_OK(hipMemcpy(d.xpow, xp.data(), xp.size() * 4, hipMemcpyHostToDevice));
+    {
+        std::vector<uint32_t> xk(mcrc_dev::kXkN);
+        const uint32_t up = mcrc::xpow8n(1), down = mcrc::xpow8n_inv(1);  // x^8, x^-8
+        uint32_t v = 0x80000000u;                                          // x^0
+        for (int32_t e = 0; e < (int32_t)mcrc_dev::kXkN + mcrc_dev::kXkLo; ++e, v = mcrc::mulmodp(v, up))
+            xk[e - mcrc_dev::kXkLo] = v;
+        v = 0x80000000u;
+        for (int32_t e = 0; e >= mcrc_dev::kXkLo; --e, v = mcrc::mulmodp(v, down)) xk[e - mcrc_dev::kXkLo] = v;
+        HIP_OK(hipMalloc(&d.xk, xk.size() * 4));
+        HIP_OK(hipMemcpy(d.xk, xk.data(), xk.size() * 4, hipMemcpyHostToDevice));
+    }
     HIP_OK(hipMalloc(&d.zero, mcrc_dev::kZeroBytes));
     HIP_OK(hipMemset(d.zero, 0, mcrc_dev::kZeroBytes));
     HIP_OK(hipMalloc(&d.nbad, 2 * sizeof(unsigned long long)));
@@ -283,6 +295,10 @@ int init_device(Device &d, int id) {
         (const void *)mcrc_dev::k_items<0, false>,
         (const void *)mcrc_dev::k_items<1, true>,
         (const void *)mcrc_dev::k_items<2, true>,
+        (const void *)mcrc_dev::k_lines<0, true>,
+        (const void *)mcrc_dev::k_lines<0, false>,
+        (const void *)mcrc_dev::k_lines<1, true>,
+        (const void *)mcrc_dev::k_lines<2, true>,
     };
     for (const void *k : k160)
         HIP_OK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mcrc_dev::kLdsImageK1Bytes));
@@ -379,15 +395,42 @@ bool one_block_len(uint32_t len) {
     return true;
 }
 
-// Every span of `len` bytes, at any alignment, is one block after a head
-// fragment of 4..kFragMax bytes (mcrc_dev::fused_vlen): k_items takes the
-// batch whole (configs 2r: 4133-B spans).
+// Every span of `len` bytes, at any alignment, has K5's fused shape: K5 takes
+// the batch whole (config 2r: 4133-B spans).  k_items: one block after a head
+// fragment of 4..kFragMax bytes (mcrc_dev::fused_vlen), at every 16-B
+// alignment; k_lines: 31 or 32 whole lines after a 4..131-B head, at every
+// 128-B alignment.
 bool fused_len(uint32_t len) {
+#if MCRC_K5_ITEMS
     for (uint32_t kh = 0; kh < 16; ++kh) {
         const uint32_t vlen = len + ((0u - kh - len) & (mcrc_dev::kTailAlign - 1));
         if (!mcrc_dev::fused_vlen(vlen)) return false;
     }
+#else
+    constexpr uint32_t L = mcrc_dev::kLineBytes;
+    for (uint32_t al = 0; al < L; ++al) {
+        const int64_t A = (al + 4 + L - 1) / L * L, B = (al + (int64_t)len) / L * L;
+        if (len < 4 || !mcrc_dev::lines_fused(B - A)) return false;
+    }
+#endif
     return true;
+}
+
+// K5's kernel for a batch of n spans or images (k_lines: runs of 2 nsr
+// consecutive images per wave, nsr up to kEpoch, enough runs for every wave).
+template <int MODE, bool OFFS>
+void launch_k5(const Device &d, const mcrc_dev::SpanArgs &a, mcrc_dev::ItemsOut io, hipStream_t st) {
+    const int grid = grid_for(d, a.n);
+#if MCRC_K5_ITEMS
+    hipLaunchKernelGGL((mcrc_dev::k_items<MODE, OFFS>), dim3(grid), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st, a,
+                       d.img, io);
+#else
+    const uint64_t waves = (uint64_t)grid * (1024 / 64);
+    io.xk = d.xk;
+    io.nsr = (uint32_t)std::min<uint64_t>(mcrc_dev::kEpoch, std::max<uint64_t>(1, (a.n + 2 * waves - 1) / (2 * waves)));
+    hipLaunchKernelGGL((mcrc_dev::k_lines<MODE, OFFS>), dim3(grid), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st, a,
+                       d.img, io);
+#endif
 }
 
 // Large item batches go through launch_items, where k_census samples their
@@ -471,13 +514,9 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
         return launch_small<MODE>(d, a, st);
     }
     if (identity && fused_len(a.len) && n < 0xffffffffull) {  // K5: one block after a head fragment
-        mcrc_dev::ItemsOut io{};  // (MODE 0: k_items stores every CRC itself)
-        if (a.offsets)
-            hipLaunchKernelGGL((mcrc_dev::k_items<0, true>), dim3(grid_for(d, n)), dim3(1024),
-                               mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
-        else
-            hipLaunchKernelGGL((mcrc_dev::k_items<0, false>), dim3(grid_for(d, n)), dim3(1024),
-                               mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
+        mcrc_dev::ItemsOut io{};  // (MODE 0: K5 stores every CRC itself)
+        if (a.offsets) launch_k5<0, true>(d, a, io, st);
+        else launch_k5<0, false>(d, a, io, st);
         HIP_OK(hipGetLastError());
         return CRC32C_OK;
     }
@@ -568,8 +607,7 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     if (!io.fb || (MODE == 2 && !io.rt) || !fo || !fok) return CRC32C_ENOMEM;
     HIP_OK(hipMemsetAsync(d.nfb, 0, 4, st));
     hipLaunchKernelGGL(mcrc_dev::k_census<MODE>, dim3(1), dim3(mcrc_dev::kCensus), 0, st, a, d.route);
-    hipLaunchKernelGGL((mcrc_dev::k_items<MODE, true>), dim3(grid_for(d, n)), dim3(1024),
-                       mcrc_dev::kLdsImageK1Bytes, st, a, d.img, io);
+    launch_k5<MODE, true>(d, a, io, st);
     const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 1024);
     if (MODE == 2)
         hipLaunchKernelGGL(mcrc_dev::k_fix, dim3(g), dim3(256), 0, st, a, (const uint2 *)io.rt,

@@ -1,0 +1,150 @@
+"""CPU restatement of K5's line-anchored form (round 4, crc32c_kernels.hip
+k_items, MCRC_K5_LINES): the block of an image starts and ends on 128-B lines,
+so no HBM line is read both by a block and by an image's per-lane prep.
+
+For span D = [p, E) with initial CRC c:
+* A = ceil128(p + 4), B = floor128(E): the image's block is the virtual
+  4 KiB window [A, A + 4096) -- the whole lines [A, B) of D, zeros past B
+  (the group's lanes whose pieces start at or past B read the zero line);
+  the shape is fused when the window holds 31 or 32 of D's lines;
+* the epoch lane takes the head [p, A) (4..131 bytes; bytes below p cleared,
+  ~c XORed into [p, p + 4): r_h = the register from ~c over [p, A)) and the
+  tail [B, Et), Et = ceil16(E), bytes from E on cleared (r_t = raw of
+  [B, E) followed by pad = Et - E zero bytes);
+* with R = raw of the window from the group's lanes,
+    V = M_{Et-A}(r_h) ^ M_{Et-A-4096}(R) ^ r_t = M_pad(f),
+  f the register after D from ~c (the second shift is negative when the
+  window runs past B: x^(8e) for e in [-128, 4352) is one table);
+* crc32c(c, D) = ~M_{-pad}(V); a verify is good iff V == M_pad(~stored).
+Checked against the oracle at every 128-B alignment of the fused lengths.
+"""
+import numpy as np
+import pytest
+
+from tests import oracle
+from tests.span_model import M32, mulmodp, xpow8, xpow8_inv
+
+LINE = 128
+BLOCK = 4096
+
+
+def reg(r, data):
+    return ~oracle.crc32c(~r & M32, bytes(data)) & M32
+
+
+def raw(data):
+    return reg(0, data)
+
+
+def zeros(v, n):
+    return oracle.lib().oracle_shift_zeros(v & M32, n)
+
+
+def xk(e):
+    """x^(8e) for -128 <= e < 4352 (the kernel's table)."""
+    assert -128 <= e < 4352
+    return xpow8(e) if e >= 0 else xpow8_inv(-e)
+
+
+def lines_shape(p, length):
+    """(A, B, fused): k_items' line-anchored shape test."""
+    A = (p + 4 + LINE - 1) // LINE * LINE
+    E = p + length
+    B = E // LINE * LINE
+    return A, B, B > A and BLOCK - LINE <= B - A <= BLOCK
+
+
+def head_dword(v, pa, inj):
+    if pa >= 4:
+        return 0
+    if pa >= 0:
+        return ((v & ((M32 << (8 * pa)) & M32)) ^ (inj << (8 * pa))) & M32
+    if pa > -4:
+        return v ^ (inj >> (8 * -pa))
+    return v
+
+
+def chain(dwords):
+    """The lane's slice-by-4 chain over a dword stream from register 0."""
+    x = 0
+    for k, d in enumerate(dwords):
+        x = d if k == 0 else zeros(x, 4) ^ d
+    return zeros(x, 4) if dwords else 0
+
+
+def head_chain(buf, p, A, inj):
+    ph = p - (p & 15)
+    dw = []
+    for a in range(ph, A, 4):
+        v = int.from_bytes(bytes(buf[a:a + 4]), "little")
+        dw.append(head_dword(v, p - a, inj))
+    return chain(dw)
+
+
+def tail_chain(buf, B, E):
+    Et = (E + 15) // 16 * 16
+    dw = []
+    for a in range(B, Et, 4):
+        b = bytearray(buf[a:a + 4])
+        for i in range(4):
+            if a + i >= E:
+                b[i] = 0
+        dw.append(int.from_bytes(bytes(b), "little"))
+    return chain(dw)
+
+
+def kernel_lines(buf, p, length, crc_in=0):
+    """(V, pad) as the line-anchored k_items computes them."""
+    A, B, fused = lines_shape(p, length)
+    assert fused
+    E = p + length
+    Et = (E + 15) // 16 * 16
+    pad = Et - E
+    inj = ~crc_in & M32
+    r_h = head_chain(buf, p, A, inj)
+    assert r_h == reg(inj, buf[p:A])
+    r_t = tail_chain(buf, B, E)
+    assert r_t == zeros(raw(buf[B:E]), pad)
+    window = bytes(buf[A:B]) + bytes(A + BLOCK - B)
+    R = raw(window)
+    V = mulmodp(r_h, xk(Et - A)) ^ mulmodp(R, xk(Et - A - BLOCK)) ^ r_t
+    return V, pad
+
+
+@pytest.mark.parametrize("al", range(0, 128, 5))
+def test_line_anchored_V_is_M_pad_of_the_register(al):
+    rng = np.random.default_rng(al)
+    buf = rng.integers(0, 256, 3 * BLOCK, dtype=np.uint8).tobytes()
+    p = 256 + al
+    for length in (4100, 4133, 4165, 4190, 4226, 4227):
+        A, B, fused = lines_shape(p, length)
+        if not fused:
+            continue
+        D = buf[p:p + length]
+        f = reg(M32, D)
+        V, pad = kernel_lines(buf, p, length)
+        assert V == zeros(f, pad)
+        crc = oracle.crc32c(0, D)
+        assert ~mulmodp(V, xpow8_inv(pad)) & M32 == crc
+        # verify: good iff V == M_pad(~stored)
+        assert V == zeros(~crc & M32, pad) and V != zeros(~(crc ^ 1) & M32, pad)
+        c = int(rng.integers(0, 1 << 32))
+        Vc, _ = kernel_lines(buf, p, length, crc_in=c)
+        assert ~mulmodp(Vc, xpow8_inv(pad)) & M32 == oracle.crc32c(c, D)
+
+
+def test_line_anchored_shapes():
+    """Every 128-B alignment of a 4133-B span (configs 2r and 5) is fused, and
+    so is every length 4100..4227; lengths whose interior holds 33 lines or
+    fewer than 31 are not; the head is 4..131 bytes, the exponents stay in
+    the table's range."""
+    for L in range(4100, 4228):
+        for al in range(128):
+            A, B, fused = lines_shape(al, L)
+            assert fused, (L, al)
+            E = al + L
+            Et = (E + 15) // 16 * 16
+            assert 4 <= A - al <= 131 and -128 <= Et - A - BLOCK and Et - A < 4352
+    assert not any(lines_shape(al, 4354)[2] and lines_shape(al, 4354)[1] - lines_shape(al, 4354)[0] > BLOCK
+                   for al in range(128))
+    assert not any(lines_shape(al, L)[2] for L in (3800, 3900, 4500) for al in range(128))

@@ -58,7 +58,7 @@ def test_every_kernel_allocates_at_least_32_vgprs(tmp_path):
     # every kernel of crc32c_kernels.hip is in the library
     for k in ("k_fixed", "k_spans", "k_count", "k_expand", "k_expand_big", "k_final", "k_small", "k_blocks",
               "k_items", "k_fix", "k_gather_offs", "k_scatter_ok", "k_chain", "k_walk", "k_plan_tiles",
-              "k_plan_scan", "k_scan32", "k_census"):
+              "k_plan_scan", "k_scan32", "k_census", "k_lines"):
         assert any(re.search(rf"\d{k}E", n) or re.search(rf"\d{k}I", n) for n in ks), k
     low = {n: v for n, (v, a, _) in ks.items() if ((v + 7) // 8) * 8 < 32}
     assert not low, f"kernels allocating fewer than 32 VGPRs: {low}"
