@@ -169,13 +169,8 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     auto ld = [&](Regs &r, uint64_t gi) {
         const uint64_t gu = gi < ngroups ? gi : gi - gstep < ngroups ? gi - gstep : ngroups - 1;
         const uint64_t first = gu * IPW;
-        // (round 4) the prefetch past the wave's last group reads the table
-        // image (L2-resident: every workgroup copied it) instead of repeating
-        // that group: the repeat came a whole step later, out of L2 again,
-        // and cost 1/128 of the launch's HBM reads
-        const bool past = gi >= ngroups;
-        const uint8_t *wb = past ? reinterpret_cast<const uint8_t *>(img) : base + first * stride;
-        const uint32_t gl = past ? 0u : first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
+        const uint8_t *wb = base + first * stride;
+        const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
         // crc_in first: it is consumed before the first chain step, and
         // vmcnt counts in issue order (issued last, it made the step wait for
         // all of its loads before any chain could start)
@@ -2059,7 +2054,7 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
     uint32_t p_kh = 0, p_inj = ~0u, p_stored = 0, p_nh = 0, p_nt = 0, p_eta = 0;
     uint64_t p_pho = 0, p_b = 0;
     uint32_t r_h = 0, r_t = 0, er = 0;
-    uint4 pc[kHeadPieces];
+    uint4 pc[kHeadPieces], tc[kTailPieces];
     auto prep_head = [&](uint64_t r) {
         const bool valid = valid_of(r);
         const uint64_t off = noff;
@@ -2118,15 +2113,13 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
     // (the last piece's bytes from E on are cleared: pad of them)
     auto tail_loads = [&]() {
 #pragma unroll
-        for (uint32_t k = 0; k < kTailPieces; ++k) {
-            pc[k] = ld16(k < p_nt ? gb + p_b + 16 * k : gz);
-        }
+        for (uint32_t k = 0; k < kTailPieces; ++k) tc[k] = ld16(k < p_nt ? gb + p_b + 16 * k : gz);
     };
     auto tail_chain = [&]() {
         uint32_t x = 0;
 #pragma unroll
         for (uint32_t k = 0; k < kTailPieces; ++k) {
-            const uint4 v = k + 1 == p_nt ? clear_high(pc[k], est & 15u) : pc[k];
+            const uint4 v = k + 1 == p_nt ? clear_high(tc[k], est & 15u) : tc[k];
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j) {
@@ -2142,10 +2135,7 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
         const int src = (int)(2 * min(s, ns - 1) + g);
         const uint64_t lo = (uint32_t)__shfl((int)eglo, src, 64), hi = (uint32_t)__shfl((int)eghi, src, 64);
         b.st = (uint32_t)__shfl((int)est, src, 64);
-        // (a step past the run -- the prefetch after its last step -- reads
-        // the workgroup's zero line: a repeat of the last step came a step
-        // later, out of L2 again, and cost 1/32 of the run's HBM reads)
-        gbyte *blk = (b.st & kStFused) && s < ns ? gb + (lo | (hi << 32)) : gz;
+        gbyte *blk = (b.st & kStFused) ? gb + (lo | (hi << 32)) : gz;
         const bool z3 = (b.st & kSt31) && li >= 28u;  // row 3 past B: zeros
 #pragma unroll
         for (int r = 0; r < 3; ++r)
@@ -2213,13 +2203,18 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
         const uint64_t left = n - r * run_imgs;
         const uint32_t ns = (uint32_t)min((uint64_t)nsr, (left + 1) / 2);
         prep_head(r);
+        // the head and tail lines of neighbouring images are the same lines:
+        // both loads at once, so one image's tail and the next image's head
+        // are fetched together (tail loads after the head chain came ~2 us
+        // later and fetched the shared line again: 1.036x for config 2r)
         head_loads();
+        tail_loads();
+        __builtin_amdgcn_sched_barrier(0);  // (not sunk towards the tail chain)
         // the next run's offsets (and initial CRCs), consumed one run later
         noff = off_of(r + W);
         if (MODE == 0) ncin = a.crc_in && valid_of(r + W) ? a.crc_in[item_of(r + W)] : 0u;
-        ld(ra, 0, ns);
         head_chain();
-        tail_loads();
+        ld(ra, 0, ns);  // (after the head chain: its registers are free again)
         tail_chain();
         er = 0;
         uint32_t s = 0;
