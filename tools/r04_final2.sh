@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-4 evidence, part 2: the page workloads (1000 x 64 MiB pages) and the
+# per-call / multi / host workloads, with kernel traces.
+#   bash tools/r04_final2.sh OUT
+source tools/gpu_guard.sh
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r04final2}; mkdir -p $O
+for w in config5 stamp pages pagesmix; do
+  a="--workload $w --pages 1000 --steps 3 --warmup 1"
+  run 600 python bench.py $a > $O/$w.json 2> $O/$w.err
+  run 600 rocprofv3 --kernel-trace --stats -d $O/kt_$w -o kt --output-format csv -- python3 bench.py --workload $w --pages 300 --steps 3 --warmup 1 > $O/kt_$w.json 2> $O/kt_$w.err
+done
+run 300 python bench.py --workload calls > $O/calls.json 2> $O/calls.err
+run 300 python bench.py --workload multi --gpus 1 --steps 20 --warmup 5 > $O/multi.json 2> $O/multi.err
+run 300 python bench.py --workload host --steps 5 --warmup 1 > $O/host.json 2> $O/host.err
+echo done
