@@ -1070,7 +1070,7 @@ struct PlanSum {
     uint64_t units, blocks;
     uint32_t fast, pad;
 };
-constexpr uint32_t kPlanThreads = 256, kPlanPer = 8, kPlanTile = kPlanThreads * kPlanPer;
+constexpr uint32_t kPlanThreads = 1024, kPlanPer = 2, kPlanTile = kPlanThreads * kPlanPer;
 
 __device__ __forceinline__ PlanSum plan_of(uint64_t nu, uint8_t f) {
     return {(uint32_t)nu, nu >> 32, (uint32_t)f, 0u};
@@ -1079,8 +1079,8 @@ __device__ __forceinline__ PlanSum plan_add(const PlanSum &x, const PlanSum &y) 
     return {x.units + y.units, x.blocks + y.blocks, x.fast + y.fast, 0u};
 }
 
-// Exclusive scan of v over a 256-thread workgroup; *total = the sum of all.
-// Every thread calls it (two barriers; `sh` holds 4 wave sums).
+// Exclusive scan of v over a kPlanThreads workgroup; *total = the sum of all.
+// Every thread calls it (two barriers; `sh` holds the wave sums).
 __device__ __forceinline__ PlanSum block_scan_excl(PlanSum v, PlanSum *sh, PlanSum *total) {
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     PlanSum inc = v;
@@ -1206,8 +1206,12 @@ struct Balance {
 __device__ __forceinline__ Balance balance_of(const PlanSum *total, uint64_t n, uint32_t groups, uint32_t *starts) {
     Balance b{starts, 1, 0};
     if (starts && n) {
+        // (at least a segment's blocks per group: a small batch -- e.g. K5's
+        // fallback list of a few long images -- would otherwise cut every
+        // unit into one record per block, serially in its span's thread of
+        // k_expand, ~0.3 ms for 50 images of 1-2 MiB)
         const uint64_t t = total->blocks;
-        b.per = max((t + groups - 1) / groups, (uint64_t)1);
+        b.per = max((t + groups - 1) / groups, (uint64_t)(kSegBytes / kBlockBytes));
         b.gm = (t + b.per - 1) / b.per;
     }
     return b;
@@ -2015,19 +2019,25 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
     // item images (verify / stamp) by offsets
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint64_t n = a.n;
-    const uint32_t nsr = io.nsr;
+    const uint64_t nsr = io.nsr;
     const uint64_t run_imgs = 2ull * nsr;
-    const uint64_t nruns = (n + run_imgs - 1) / run_imgs;
     const uint64_t waves = blockDim.x >> 6;
     const uint64_t W = gridDim.x * waves;
     const uint64_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
-    if ((uint64_t)blockIdx.x * waves >= nruns) return;
+    // Runs: round k of wave w is the run of 2 nsr consecutive images from
+    // (k W + w) 2 nsr.  (Staggering the waves' first runs, so that their
+    // run starts -- header, head and tail loads, two chains, no window in
+    // flight -- do not coincide on a CU, unbalanced the waves and was 1-9 %
+    // slower: profiles/r04_ablations/k5_lines_stagger_ab.txt.)
+    auto run_start = [&](uint64_t k) -> uint64_t { return (k * W + w0) * run_imgs; };
+    auto run_steps = [&](uint64_t) -> uint64_t { return nsr; };
+    if ((uint64_t)blockIdx.x * waves * run_imgs >= n) return;
     if (MODE != 0 && io.route && *io.route == 0) {  // the census sent the batch to the planned path
         if (blockIdx.x == 0 && threadIdx.x == 0) *io.nfb = (uint32_t)n;
         return;
     }
     load_tables(smem, img, kLdsImageK1Bytes);
-    if (w0 >= nruns) return;
+    if (run_start(0) >= n) return;
     const uint32_t lane = threadIdx.x & 63u, li = lane & 31u, g = lane >> 5;
     LaneCtx c;
     c.lane4 = li << 2;
@@ -2037,8 +2047,9 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
     const uint32_t base_lo = (uint32_t)(uintptr_t)a.base;  // (alignments: the offsets are from a.base)
     uint32_t nb = 0;  // bad (malformed or mismatching) images seen by this lane
 
-    auto item_of = [&](uint64_t r) -> uint64_t { return r * run_imgs + lane; };
-    auto valid_of = [&](uint64_t r) { return lane < run_imgs && r < nruns && item_of(r) < n; };
+    // (r: the wave's round, 0, 1, 2, ...)
+    auto item_of = [&](uint64_t r) -> uint64_t { return run_start(r) + lane; };
+    auto valid_of = [&](uint64_t r) { return lane < 2 * run_steps(r) && item_of(r) < n; };
     auto off_of = [&](uint64_t r) -> uint64_t {
         // (offsets or stride is a template choice: a load on one side of a
         // branch leaves the waitcnt pass a merged state that waits for it)
@@ -2046,8 +2057,8 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
     };
     // MODE 0: x^(-8t), t < 16, lane-distributed (lane j holds t = j & 15)
     const uint32_t xinv = MODE == 0 ? a.xpow[kXpowInv + (lane & 15u)] : 0u;
-    uint64_t noff = off_of(w0);  // this lane's image offset in the wave's next run
-    uint32_t ncin = MODE == 0 && a.crc_in && valid_of(w0) ? a.crc_in[item_of(w0)] : 0u;
+    uint64_t noff = off_of(0);  // this lane's image offset in the wave's next run
+    uint32_t ncin = MODE == 0 && a.crc_in && valid_of(0) ? a.crc_in[item_of(0)] : 0u;
 
     // this lane's image of the run
     uint32_t eglo = 0, eghi = 0, est = 0;  // window start A (offset from a.base), status
@@ -2199,9 +2210,9 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
         }
     };
     ItemBuf ra, rb;
-    for (uint64_t r = w0; r < nruns; r += W) {
-        const uint64_t left = n - r * run_imgs;
-        const uint32_t ns = (uint32_t)min((uint64_t)nsr, (left + 1) / 2);
+    for (uint64_t r = 0; run_start(r) < n; ++r) {
+        const uint64_t left = n - run_start(r);
+        const uint32_t ns = (uint32_t)min(run_steps(r), (left + 1) / 2);
         prep_head(r);
         // the head and tail lines of neighbouring images are the same lines:
         // both loads at once, so one image's tail and the next image's head
@@ -2211,8 +2222,8 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
         tail_loads();
         __builtin_amdgcn_sched_barrier(0);  // (not sunk towards the tail chain)
         // the next run's offsets (and initial CRCs), consumed one run later
-        noff = off_of(r + W);
-        if (MODE == 0) ncin = a.crc_in && valid_of(r + W) ? a.crc_in[item_of(r + W)] : 0u;
+        noff = off_of(r + 1);
+        if (MODE == 0) ncin = a.crc_in && valid_of(r + 1) ? a.crc_in[item_of(r + 1)] : 0u;
         head_chain();
         ld(ra, 0, ns);  // (after the head chain: its registers are free again)
         tail_chain();

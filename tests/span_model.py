@@ -192,7 +192,7 @@ def balanced_plan(spans, groups):
         for up, eo, nb, single, segk in units_of(0, p, length):
             units.append((s, (up, eo, nb, single, SEG_BLOCKS * segk)))
     t = sum(u[2] for _, u in units)
-    per = max(-(-t // groups), 1)
+    per = max(-(-t // groups), SEG_BLOCKS)  # (k_expand: at least a segment's blocks per group)
     gm = -(-t // per)
     starts = {0: 0}
     records = []

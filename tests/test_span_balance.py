@@ -57,7 +57,7 @@ def test_groups_get_equal_contiguous_block_ranges(groups):
     want = [(s, b) for s, (p, length) in enumerate(spans) for u in units_of(0, p, length)
             for b in blocks_of((u[0], u[1], u[2], u[3], 0))]
     t = len(want)
-    assert per == max(-(-t // groups), 1)
+    assert per == max(-(-t // groups), SEG // BLOCK)  # (a segment's blocks at least)
     got = []
     for g in range(groups):
         if g * per >= t:
