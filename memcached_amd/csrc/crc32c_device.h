@@ -98,6 +98,11 @@ constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 #ifndef MCRC_K5_ITEMS
 #define MCRC_K5_ITEMS 0
 #endif
+// k_lines: a contiguous chunk of images per wave with staggered runs (0: the
+// round-robin runs of the first k_lines, kept for A/B)
+#ifndef MCRC_K5_CHUNK
+#define MCRC_K5_CHUNK 1
+#endif
 // Nibble form of the shifted tables (MCRC_NIB): set s (row chain s, shift
 // M_{(3-s)*1024}) holds 8 tables of 16 entries, table 2k + h for nibble h of
 // byte k, at kNibShiftBytes + 512 s + 64 (2k + h).  A 16-entry table spans 16

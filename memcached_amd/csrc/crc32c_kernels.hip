@@ -2024,20 +2024,35 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
     const uint64_t waves = blockDim.x >> 6;
     const uint64_t W = gridDim.x * waves;
     const uint64_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
-    // Runs: round k of wave w is the run of 2 nsr consecutive images from
-    // (k W + w) 2 nsr.  (Staggering the waves' first runs, so that their
-    // run starts -- header, head and tail loads, two chains, no window in
-    // flight -- do not coincide on a CU, unbalanced the waves and was 1-9 %
+    // Runs: wave w checksums the contiguous chunk [w C, (w + 1) C) of images
+    // (C = ceil(n / W) rounded up to even), as a first run of 1 + (w % nsr)
+    // steps and then runs of nsr steps: the same work on every wave, the
+    // waves' run starts spread over nsr steps, and a wave's consecutive runs
+    // read consecutive lines (config 5 -2.5 %, configs 2r / stamp within
+    // noise, against round k of wave w being the run from (k W + w) 2 nsr:
+    // profiles/r04_ablations/k5_lines_chunk_ab.txt).  (Staggering only the
+    // first runs of the round-robin order unbalanced the waves and was 1-9 %
     // slower: profiles/r04_ablations/k5_lines_stagger_ab.txt.)
+    // tests/test_items_lines_model.py checks that the runs cover every image
+    // exactly once.
+#if MCRC_K5_CHUNK
+    const uint64_t C = ((n + W - 1) / W + 1) & ~1ull;
+    const uint64_t f0 = 1 + w0 % nsr, cend = min((w0 + 1) * C, n);
+    auto run_start = [&](uint64_t k) -> uint64_t { return w0 * C + (k == 0 ? 0 : 2 * (f0 + (k - 1) * nsr)); };
+    auto run_steps = [&](uint64_t k) -> uint64_t { return k == 0 ? f0 : nsr; };
+    if ((uint64_t)blockIdx.x * waves * C >= n) return;
+#else
     auto run_start = [&](uint64_t k) -> uint64_t { return (k * W + w0) * run_imgs; };
     auto run_steps = [&](uint64_t) -> uint64_t { return nsr; };
+    const uint64_t cend = n;
     if ((uint64_t)blockIdx.x * waves * run_imgs >= n) return;
+#endif
     if (MODE != 0 && io.route && *io.route == 0) {  // the census sent the batch to the planned path
         if (blockIdx.x == 0 && threadIdx.x == 0) *io.nfb = (uint32_t)n;
         return;
     }
     load_tables(smem, img, kLdsImageK1Bytes);
-    if (run_start(0) >= n) return;
+    if (run_start(0) >= cend) return;
     const uint32_t lane = threadIdx.x & 63u, li = lane & 31u, g = lane >> 5;
     LaneCtx c;
     c.lane4 = li << 2;
@@ -2049,7 +2064,7 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
 
     // (r: the wave's round, 0, 1, 2, ...)
     auto item_of = [&](uint64_t r) -> uint64_t { return run_start(r) + lane; };
-    auto valid_of = [&](uint64_t r) { return lane < 2 * run_steps(r) && item_of(r) < n; };
+    auto valid_of = [&](uint64_t r) { return lane < 2 * run_steps(r) && item_of(r) < cend; };
     auto off_of = [&](uint64_t r) -> uint64_t {
         // (offsets or stride is a template choice: a load on one side of a
         // branch leaves the waitcnt pass a merged state that waits for it)
@@ -2210,8 +2225,8 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
         }
     };
     ItemBuf ra, rb;
-    for (uint64_t r = 0; run_start(r) < n; ++r) {
-        const uint64_t left = n - run_start(r);
+    for (uint64_t r = 0; run_start(r) < cend; ++r) {
+        const uint64_t left = cend - run_start(r);
         const uint32_t ns = (uint32_t)min(run_steps(r), (left + 1) / 2);
         prep_head(r);
         // the head and tail lines of neighbouring images are the same lines:
