@@ -676,6 +676,7 @@ def extra_workload(args):
         if args.items == ITEMS_PER_GPU:
             args.items = 1 << 20
         spans, nbytes, cfg = workload_config3(args, rank, world)
+        res["settle_launches"] = settle(lambda k: run_steps(spans, k, stream), args.settle_ms)
         run_steps(spans, max(1, args.warmup), stream)
         torch.cuda.synchronize()
         elapsed, evs = timed(lambda k: run_steps(spans, k, stream), args.steps, world)
@@ -685,6 +686,7 @@ def extra_workload(args):
     elif args.workload in ("config5", "pagesmix"):
         vargs, ok, victims, nbytes, cfg = (workload_config5 if args.workload == "config5" else
                                            workload_pagesmix)(args, rank, world)
+        res["settle_launches"] = settle(lambda k: run_verify_steps(vargs, k, stream), args.settle_ms)
         run_verify_steps(vargs, max(1, args.warmup), stream)
         torch.cuda.synchronize()
         elapsed, (evs, nbad) = timed(lambda k: run_verify_steps(vargs, k, stream), args.steps, world)
@@ -701,6 +703,7 @@ def extra_workload(args):
         data = torch.randint(0, 256, (n * (sl + 32) + 64,), dtype=torch.uint8, device="cuda", generator=g)
         out = torch.empty(n, dtype=torch.int32, device="cuda")
         spans = _lib.Spans(data.data_ptr() + 32, data.numel() - 32, None, sl + 32, None, sl, None, out.data_ptr(), n)
+        res["settle_launches"] = settle(lambda k: run_steps(spans, k, stream), args.settle_ms)
         run_steps(spans, max(1, args.warmup), stream)
         torch.cuda.synchronize()
         elapsed, evs = timed(lambda k: run_steps(spans, k, stream), args.steps, world)
@@ -737,6 +740,7 @@ def extra_workload(args):
                 b.record(stream)
             return evs
 
+        res["settle_launches"] = settle(steps, args.settle_ms)
         steps(max(1, args.warmup))
         torch.cuda.synchronize()
         elapsed, evs = timed(steps, args.steps, world)
