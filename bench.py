@@ -342,7 +342,7 @@ def workload_config5(args, rank, world):
     return (data.data_ptr(), data.numel(), wbuf, offs.data_ptr(), n, ok.data_ptr()), ok, victims, \
         n * (ntotal - 32), {
             "workload": f"BASELINE configs[4]: {args.pages} x 64 MiB extstore pages, 16 wbufs x 1007 packed "
-                        "4165-B item images each, stored CRC verified per item (K5 k_items<verify>; other shapes "
+                        "4165-B item images each, stored CRC verified per item (K5 k_lines<verify>; other shapes "
                         "through the planned K3 path)",
             "pages_per_gpu": args.pages, "items_per_gpu": n, "span_bytes_per_gpu": n * (ntotal - 32),
             "injected_bad": int(victims.numel())}
@@ -710,7 +710,7 @@ def extra_workload(args):
         kms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
         nbytes = n * sl
         res.update(config={"workload": f"config 2 variant: {n} x {sl}-B spans at stride {sl + 32}, start +32 "
-                                       "(K5 k_items: one 4 KiB block after a head fragment per span, + k_fix)"},
+                                       "(K5 k_lines: 31-32 whole 128-B lines per span in one 4 KiB window, head and tail by the span's run lane)"},
                    kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
                    hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
     elif args.workload in ("pages", "stamp"):

@@ -147,7 +147,9 @@ int crc32c_batch_chains(const crc32c_spans *iovs, const uint64_t *chain_first, u
  * cap == 0 is a count-only query: the walk runs, nothing is verified, *nbad =
  * 0 and offsets / ok may be NULL.  An item count is at most
  * base_bytes / 50 + ceil(base_bytes / wbuf_bytes) (an image is >= 50 bytes; a
- * wbuf's last counted image may run past its end). */
+ * wbuf's last counted image may run past its end).  Device scratch: the walk
+ * keeps up to wbuf_bytes / 2048 offsets per wbuf (8 B each, 0.4 % of the
+ * walked bytes; grow-only, reused by later calls). */
 int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_bytes,
                         uint64_t *offsets, uint8_t *ok, uint64_t cap, uint64_t *nitems,
                         uint64_t *nbad, unsigned flags, void *stream);
