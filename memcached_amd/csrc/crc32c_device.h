@@ -103,6 +103,14 @@ constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 #ifndef MCRC_K5_CHUNK
 #define MCRC_K5_CHUNK 1
 #endif
+// k_lines stamps (MODE 2): the epoch lane stores each fused image's CRC itself
+// (1) instead of leaving {V, pad} for k_fix (0)
+#ifndef MCRC_ABL_COUNT  // (k_count timing ablation; 0 in every product build)
+#define MCRC_ABL_COUNT 0
+#endif
+#ifndef MCRC_K5_STAMP
+#define MCRC_K5_STAMP 0
+#endif
 // Nibble form of the shifted tables (MCRC_NIB): set s (row chain s, shift
 // M_{(3-s)*1024}) holds 8 tables of 16 entries, table 2k + h for nibble h of
 // byte k, at kNibShiftBytes + 512 s + 64 (2k + h).  A 16-entry table spans 16

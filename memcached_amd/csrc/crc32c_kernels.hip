@@ -1039,6 +1039,12 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
     const uint64_t off = (uint64_t)(it.p - a.base);
     uint32_t z = 0;
     if (it.sane) {
+#if MCRC_ABL_COUNT  // (ablation, wrong results: 1 = whole spans' chains skipped, 2 = every chain skipped)
+        const SpanHead hh = span_head(it.p, it.len);
+        const bool whole = hh.drop && hh.g1o == (uint64_t)it.len + tail_pad(it.p, it.len);
+        if (MCRC_ABL_COUNT == 2 || whole) z = it.len;
+        else
+#endif
         z = span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow);
         if (MODE == 1) z ^= t8.zeros(~it.aux, tail_pad(it.p, it.len));  // W
     }
@@ -1050,8 +1056,11 @@ template <int MODE>
 __global__ void k_count(SpanArgs a, uint64_t *nunit, uint4 *irec, uint8_t *fast) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     __shared__ __attribute__((aligned(16))) uint32_t s8[kTab8Dwords];
-    const Tab8 t8 = load_tab8(s8, a.tab8);
     const uint64_t n = span_count(a);
+    // (a K5 fallback list is usually a few hundred spans on a grid sized for
+    // the batch: the workgroups past it leave before copying 20 KiB of tables)
+    if ((uint64_t)blockIdx.x * blockDim.x >= n) return;
+    const Tab8 t8 = load_tab8(s8, a.tab8);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         count_item<MODE>(a, i, fetch_item<MODE>(a, i), t8, nunit, irec, fast);
 }
@@ -2205,7 +2214,16 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
                     nb += !good;
                 }
             } else {
+#if MCRC_K5_STAMP && !MCRC_K5_ITEMS
+                if (fused) {
+                    const uint32_t crc = ~mulmodp_dev(v, io.xk[0u - pad - (uint32_t)kXkLo]);
+                    uint8_t *const at = const_cast<uint8_t *>(a.base) + p_pho + p_kh - 4;  // exptime
+                    __builtin_memcpy(at, &crc, 4);
+                    if (a.ok) a.ok[item] = 1;
+                }
+#else
                 io.rt[item] = fused ? make_uint2(v, pad | kRtFused) : make_uint2(0u, 0u);
+#endif
                 if (!sane) {
                     if (a.ok) a.ok[item] = 0;
                     ++nb;
@@ -2387,6 +2405,11 @@ __global__ void k_chain(const uint32_t *iov_crc, const uint32_t *lens, uint32_t 
 //   k_walk<true>: walk again and write item prefix[w] + c's offset and, for a
 //     planned verify, its plan entries (count_item: what k_count would write
 //     after reading the header a second time), so no k_count pass follows.
+// Round 4: the count pass also keeps the first kslot offsets of each wbuf
+// (out.slots), and the emit pass of a verify that needs offsets only (K5)
+// copies them instead of walking a wbuf again (the second walk re-read every
+// header line from HBM: 0.15 ms per 300 pages); a wbuf of more than kslot
+// items is walked again as before.
 // One wave per wbuf.  The walk is a dependent chain, so each round trip
 // guesses: lane j reads the header at off + j * s, s = the last item's
 // ITEM_ntotal.  Lane j's guess is right iff every lane before it holds an item
@@ -2406,6 +2429,8 @@ struct WalkOut {
     uint4 *irec;
     uint8_t *fast;
     unsigned long long *err; // emit pass: wbufs whose two walks disagree (must stay 0)
+    uint64_t *slots;         // count pass: the first kslot item offsets of wbuf w at w * kslot
+    uint32_t kslot;          // (0: none kept)
 };
 
 // a: base, base_bytes (the walked bytes), region (= wbuf), and for the plan
@@ -2432,6 +2457,10 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
         // same number of items (the walk invariant; see DESIGN.md section 3 on
         // the round-2 readlane variants that broke it)
         const uint64_t expect = EMIT ? out.prefix[w + 1] - first : 0;
+        if (EMIT && !plan && out.slots && expect <= out.kslot) {  // the count pass kept them all
+            for (uint64_t i = j; i < expect; i += 64) out.offs[first + i] = out.slots[w * out.kslot + i];
+            continue;
+        }
         uint64_t off = 0, s = 0;  // wave-uniform: next item, stride guess (0: none yet)
         uint32_t c = 0;           // items walked so far
         while (off + 48 <= size) {
@@ -2454,6 +2483,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
             const uint64_t nt_m = (uint64_t)(uint32_t)__shfl((int)(uint32_t)nt, src, 64) |
                                   ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(nt >> 32), src, 64) << 32);
             const uint32_t k = m < 64u ? m + (last_item ? 1u : 0u) : 64u;  // items this round trip
+            if (!EMIT && out.slots && j < k && c + j < out.kslot) out.slots[w * out.kslot + c + j] = start + o;
             if (EMIT && j < k && c + j < expect) {
                 const uint64_t i = first + c + j;
                 out.offs[i] = start + o;

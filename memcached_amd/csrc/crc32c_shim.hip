@@ -68,6 +68,10 @@ static_assert(mcrc_dev::kK1CH == mcrc_dev::kSpanCH, "K1 and the span kernels sha
 thread_local float g_last_kernel_ms = -1.0f;
 
 struct Queue;
+enum {
+    kScrWalkCnt, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage, kScrItemOffs, kScrItemOut,
+    kScrFb, kScrFbOffs, kScrFbOk, kScrRt, kScrWalkSlots, kScrCount
+};
 
 struct Device {
     int id = -1;
@@ -131,7 +135,7 @@ struct Device {
     struct Scratch {
         void *p = nullptr;
         size_t bytes = 0;
-    } scratch[12];
+    } scratch[kScrCount];
     void *grow(int slot, size_t bytes) {
         Scratch &s = scratch[slot];
         if (s.bytes < bytes) {
@@ -166,10 +170,6 @@ struct Device {
         *dv = s.d;
         return true;
     }
-};
-enum {
-    kScrWalkCnt, kScrWalkPrefix, kScrWalkOffs, kScrWalkOk, kScrWalkScan, kScrStage, kScrItemOffs, kScrItemOut,
-    kScrFb, kScrFbOffs, kScrFbOk, kScrRt
 };
 enum { kPinStage, kPinOffs, kPinOk, kPinCrc };
 
@@ -609,7 +609,7 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     hipLaunchKernelGGL(mcrc_dev::k_census<MODE>, dim3(1), dim3(mcrc_dev::kCensus), 0, st, a, d.route);
     launch_k5<MODE, true>(d, a, io, st);
     const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 1024);
-    if (MODE == 2)
+    if (MODE == 2 && !(MCRC_K5_STAMP && !MCRC_K5_ITEMS))
         hipLaunchKernelGGL(mcrc_dev::k_fix, dim3(g), dim3(256), 0, st, a, (const uint2 *)io.rt,
                            (const uint32_t *)d.route);
     hipLaunchKernelGGL(mcrc_dev::k_gather_offs, dim3(g), dim3(256), 0, st, a.offsets, (const uint32_t *)io.fb,
@@ -1569,6 +1569,12 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     const dim3 bw(64 * mcrc_dev::kWalkWaves);
     mcrc_dev::WalkOut wo{};
     wo.cnt = cnt;
+    // the count pass keeps each wbuf's first offsets (one per 2 KiB of wbuf:
+    // every 4 MiB wbuf of items of at least 2 KiB), so a K5 verify's emit pass
+    // copies them instead of walking again
+    wo.kslot = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(wbuf_bytes / 2048, 64), 8192);
+    wo.slots = (uint64_t *)d->grow(kScrWalkSlots, (size_t)nw * wo.kslot * 8);
+    if (!wo.slots) wo.kslot = 0;
     HIP_OK(hipMemsetAsync(cnt + nw, 0, 4, st));
     hipLaunchKernelGGL(mcrc_dev::k_walk<false>, dim3(gw), bw, 0, st, a, nw, wo);
     hipLaunchKernelGGL(mcrc_dev::k_scan32, dim3(1), dim3(1024), 0, st, (const uint32_t *)cnt, nw + 1, prefix);
