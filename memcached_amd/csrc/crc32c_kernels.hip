@@ -450,7 +450,10 @@ __device__ __forceinline__ Piece clear_below(Piece v, uint32_t k) {
 // (leading zeros leave a zero register unchanged), so
 //   r' = M_m(r) ^ raw16(the m bytes at the top).
 // Every load is an aligned piece holding a byte of [p, p + n).
-constexpr int kAdvUnroll = 4;
+#ifndef MCRC_ADV_UNROLL
+#define MCRC_ADV_UNROLL 4
+#endif
+constexpr int kAdvUnroll = MCRC_ADV_UNROLL;
 __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, uint32_t n, const Tab8 &t) {
     if (n == 0) return r;
     const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
@@ -527,6 +530,18 @@ __device__ __forceinline__ bool one_block(const uint8_t *p, uint32_t len, const 
 //   head piece's first kh bytes moved to its top (leading zeros leave a zero
 //   register unchanged), raw(F_t) = raw of the t bytes after E.
 // One thread.
+// Z when the kernel's R covers the pieces [ph, Ea) as they lie (the third
+// case above; also k_count's wave-cooperative whole spans, whole_chunks).
+__device__ __forceinline__ uint32_t span_corr_pieces(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
+                                                     const uint32_t *xp) {
+    const uint32_t t = tail_pad(p, len);
+    const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
+    uint32_t y = ~c;
+    if (kh) y ^= raw16(shl_bytes(ld_piece(p - kh), 16 - kh), t8);  // raw(F_h)
+    uint32_t z = mulmodp_dev(y, xpow8_dev(xp, (uint64_t)len + t));
+    if (t) z ^= reg_advance(0u, p + len, t, t8);  // raw(F_t)
+    return z;
+}
 __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
                                               const uint32_t *xp) {
     const uint32_t t = tail_pad(p, len);
@@ -534,17 +549,10 @@ __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, ui
     const uint64_t vlen = (uint64_t)len + t;
     const SpanHead h = span_head(p, len);
     if (h.drop && h.g1o == vlen) return t8.zeros(reg_advance(~c, p, len, t8), t);
-    uint32_t z;
-    if (h.drop) {
-        // Ea - G1 is whole blocks; one block (every one-block span) is a table step
-        const uint32_t r = reg_advance(~c, p, (uint32_t)h.g1o, t8);
-        z = vlen - h.g1o == kBlockBytes ? t8.block(r) : mulmodp_dev(r, xpow8_dev(xp, vlen - h.g1o));
-    } else {
-        const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
-        uint32_t y = ~c;
-        if (kh) y ^= raw16(shl_bytes(ld_piece(p - kh), 16 - kh), t8);
-        z = mulmodp_dev(y, xpow8_dev(xp, vlen));
-    }
+    if (!h.drop) return span_corr_pieces(p, len, c, t8, xp);
+    // Ea - G1 is whole blocks; one block (every one-block span) is a table step
+    const uint32_t r = reg_advance(~c, p, (uint32_t)h.g1o, t8);
+    uint32_t z = vlen - h.g1o == kBlockBytes ? t8.block(r) : mulmodp_dev(r, xpow8_dev(xp, vlen - h.g1o));
     if (t) z ^= reg_advance(0u, p + len, t, t8);  // raw(F_t)
     return z;
 }
@@ -1028,7 +1036,8 @@ __device__ __forceinline__ uint32_t span_blocks(const uint8_t *p, uint32_t len, 
 // Span i's plan entries: one-block flag, unit count, item record, R = 0.
 template <int MODE>
 __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const ItemDesc &it, const Tab8 &t8,
-                                           uint64_t *nunit, uint4 *irec, uint8_t *fast) {
+                                           uint64_t *nunit, uint4 *irec, uint8_t *fast, bool whole = false,
+                                           uint32_t rwhole = 0u) {
     // a span whose unit is one whole block goes to k_blocks (no units)
     const uint8_t *g1;
     bool none;
@@ -1041,28 +1050,99 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
     if (it.sane) {
 #if MCRC_ABL_COUNT  // (ablation, wrong results: 1 = whole spans' chains skipped, 2 = every chain skipped)
         const SpanHead hh = span_head(it.p, it.len);
-        const bool whole = hh.drop && hh.g1o == (uint64_t)it.len + tail_pad(it.p, it.len);
-        if (MCRC_ABL_COUNT == 2 || whole) z = it.len;
+        const bool wh = hh.drop && hh.g1o == (uint64_t)it.len + tail_pad(it.p, it.len);
+        if (MCRC_ABL_COUNT == 2 || wh) z = it.len;
         else
 #endif
-        z = span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow);
+        // (a whole span's R from the wave, whole_chunks: z = R ^ Z of its pieces)
+        z = whole ? rwhole ^ span_corr_pieces(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow)
+                  : span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow);
         if (MODE == 1) z ^= t8.zeros(~it.aux, tail_pad(it.p, it.len));  // W
     }
     irec[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32) | (it.sane ? 0u : kInsane), it.len, z);
     a.span_acc[i] = 0u;
 }
 
+// R = raw of [ph, Ea) (the pieces as they lie) for every lane of the wave
+// whose span is whole (span_corr's first case: the thread's alone).  A whole
+// span's chain used to run in its lane while the lanes without one idled
+// (one whole span in seven on the mixed pages: 0.11 of k_count's 0.21 ms);
+// now the wave cuts the pieces of all its whole spans into 64-B chunks and
+// every lane takes one: r_c = raw of its <= 4 pieces, shifted past the rest of
+// its span (M_{Ea - end}, x^(8 n) from the xpow table), XORed into the span's
+// slot (LDS, wave-private).  tests/test_count_whole_model.py restates it.
+constexpr uint32_t kCountThreads = 256;
+__device__ __forceinline__ uint32_t whole_chunks(gbyte *gb, bool whole, uint64_t ph, uint64_t ea, const Tab8 &t,
+                                                 const uint32_t *xp, uint32_t *slot) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nch = whole ? (uint32_t)((ea - ph + 63u) >> 6) : 0u;
+    uint32_t inc = nch;  // inclusive chunk count over the wave
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)inc, d, 64);
+        if (lane >= d) inc += v;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64), excl = inc - nch;
+    slot[lane] = 0u;
+    for (uint32_t base = 0; base < total; base += 64u) {
+        const uint32_t q = base + lane;
+        // owner = the first lane whose inclusive count exceeds q
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1)
+            if ((uint32_t)__shfl((int)inc, (int)(s + step - 1u), 64) <= q) s += step;
+        const uint32_t c = q - (uint32_t)__shfl((int)excl, (int)s, 64);
+        const uint64_t sph = (uint32_t)__shfl((int)(uint32_t)ph, (int)s, 64) |
+                             ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ph >> 32), (int)s, 64) << 32);
+        const uint64_t sea = (uint32_t)__shfl((int)(uint32_t)ea, (int)s, 64) |
+                             ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ea >> 32), (int)s, 64) << 32);
+        const bool act = q < total;
+        const uint64_t c0 = sph + 64ull * c;
+        const uint32_t np = act ? (uint32_t)min((sea - c0) >> 4, (uint64_t)4) : 0u;
+        Piece pc[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) pc[k] = k < np ? ld_piece(gb + c0 + 16u * k) : Piece{0, 0};
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t nx = t.piece(r, pc[k]);
+            r = k < np ? nx : r;
+        }
+        const uint64_t after = act ? sea - (c0 + 16u * np) : 0u;
+        r = after ? mulmodp_dev(r, xpow8_dev(xp, after)) : r;
+        if (act) atomicXor(&slot[s], r);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    return whole ? slot[lane] : 0u;
+}
+
 template <int MODE>
-__global__ void k_count(SpanArgs a, uint64_t *nunit, uint4 *irec, uint8_t *fast) {
+__global__ __launch_bounds__(kCountThreads) void k_count(SpanArgs a, uint64_t *nunit, uint4 *irec, uint8_t *fast) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     __shared__ __attribute__((aligned(16))) uint32_t s8[kTab8Dwords];
+    __shared__ uint32_t wslot[kCountThreads / 64][64];
     const uint64_t n = span_count(a);
     // (a K5 fallback list is usually a few hundred spans on a grid sized for
     // the batch: the workgroups past it leave before copying 20 KiB of tables)
     if ((uint64_t)blockIdx.x * blockDim.x >= n) return;
     const Tab8 t8 = load_tab8(s8, a.tab8);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        count_item<MODE>(a, i, fetch_item<MODE>(a, i), t8, nunit, irec, fast);
+    gbyte *const gb = (gbyte *)a.base;
+    uint32_t *const slot = wslot[threadIdx.x >> 6];
+    const uint64_t lane = threadIdx.x & 63u;
+    // (a wave-uniform loop: every lane takes part in whole_chunks)
+    for (uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x - lane); i0 < n;
+         i0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = i0 + lane;
+        const bool valid = i < n;
+        ItemDesc it{a.base, 0u, 0u, false};
+        if (valid) it = fetch_item<MODE>(a, i);
+        const uint32_t t = tail_pad(it.p, it.len);
+        const uint64_t kh = (uintptr_t)it.p & 15u, off = (uint64_t)(it.p - a.base);
+        const SpanHead h = span_head(it.p, it.len);
+        const bool whole = valid && it.sane && it.len != 0 && h.drop && h.g1o == (uint64_t)it.len + t;
+        const uint32_t r = whole_chunks(gb, whole, off - kh, off + it.len + t, t8, a.xpow, slot);
+        if (valid) count_item<MODE>(a, i, it, t8, nunit, irec, fast, whole, r);
+    }
 }
 
 // ---------------------------------------------------------------------------
