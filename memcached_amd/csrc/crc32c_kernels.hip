@@ -1270,7 +1270,16 @@ __global__ __launch_bounds__(1024) void k_scan32(const uint32_t *in, uint64_t m,
 // as one unit each by a second pass; *nvalid = records written before the
 // first such span (zeroed by the caller: none fit).  Spans of more than kExpandInline segments are listed in `big`
 // and expanded by k_expand_big, one workgroup per span.
-constexpr uint32_t kExpandInline = 32;
+#ifndef MCRC_EXPAND_INLINE
+#define MCRC_EXPAND_INLINE 32
+#endif
+constexpr uint32_t kExpandInline = MCRC_EXPAND_INLINE;
+// A device-counted list (K5's fallback: a few hundred images whose length
+// bits flipped) lands in one or two tiles, so its long spans go to
+// k_expand_big sooner: k_expand 0.031 -> 0.012 ms per 300-page verify; at 8
+// for every batch config 3 got 2.4 % slower
+// (profiles/r04_ablations/k_expand_inline_ab.txt).
+constexpr uint32_t kExpandInlineDn = 8;
 
 // First segment of span i that is a unit (1 when the head segment is not).
 __device__ __forceinline__ uint32_t first_seg(const uint8_t *p, uint32_t len, uint32_t nunit) {
@@ -1367,7 +1376,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_expand(const uint8_t *base, co
             const bool sane = !(r.y & kInsane);
             if (p0 + ns <= cap) {
                 const uint32_t s0 = first_seg(base + off, r.z, (uint32_t)ns);
-                if (ns > kExpandInline) {
+                if (ns > (dn ? kExpandInlineDn : kExpandInline)) {
                     big[atomicAdd(nbig, 1u)] = make_uint4((uint32_t)i, (uint32_t)p0, (uint32_t)b0, (uint32_t)(b0 >> 32));
                 } else {
                     uint64_t bs = b0;
