@@ -359,7 +359,10 @@ def workload_pagesmix(args, rank, world):
     import numpy as np
     wbuf, nwb = 4 << 20, args.pages * 16
     rng = np.random.default_rng(17 + rank)
-    vals = np.exp(rng.uniform(np.log(512), np.log(65536), (nwb, 1024))).astype(np.int64)
+    if args.workload == "mixed41":  # 2 KiB and 6 KiB values in turn: the average image is K5's ~4.2 KiB
+        vals = np.broadcast_to(np.where(np.arange(1024) % 2, 2048, 6150), (nwb, 1024)).astype(np.int64)
+    else:
+        vals = np.exp(rng.uniform(np.log(512), np.log(65536), (nwb, 1024))).astype(np.int64)
     ntot = vals + 2 + 48 + 10 + 1 + 8                    # value + CRLF, header, key + NUL, CAS
     ends = np.cumsum(ntot, axis=1)
     keep = ends <= wbuf
@@ -411,8 +414,9 @@ def workload_pagesmix(args, rank, world):
     _KEEP.extend((data, offs))
     span_bytes = int((ntot_np - 32).sum())
     return (data.data_ptr(), data.numel(), wbuf, offs.data_ptr(), n, ok.data_ptr()), ok, victims, span_bytes, {
-        "workload": f"{args.pages} x 64 MiB extstore pages of mixed items (values log-uniform 512 B - 64 KiB, "
-                    f"mean item {int(ntot_np.mean())} B), packed per 4 MiB wbuf, stored CRC verified per item",
+        "workload": f"{args.pages} x 64 MiB extstore pages of mixed items (values "
+                    + ("2048 and 6150 B in turn" if args.workload == "mixed41" else "log-uniform 512 B - 64 KiB")
+                    + f", mean item {int(ntot_np.mean())} B), packed per 4 MiB wbuf, stored CRC verified per item",
         "pages_per_gpu": args.pages, "items_per_gpu": n, "span_bytes_per_gpu": span_bytes,
         "items_le_4k_frac": round(float((ntot_np <= 4096).mean()), 3), "injected_bad": int(victims.numel())}
 
@@ -449,8 +453,8 @@ def main(argv=None):
     ap.add_argument("--fill", default="splitmix", choices=["splitmix", "randint"],
                     help="item bytes: splitmix64(42 + rank) words (SURVEY.md 8d) or torch.randint")
     ap.add_argument("--workload", default="config2",
-                    choices=["config2", "config2r", "config3", "config5", "pagesmix", "pages", "stamp", "host", "calls",
-                             "multi"],
+                    choices=["config2", "config2r", "config3", "config5", "pagesmix", "mixed41", "pages", "stamp", "host",
+                             "calls", "multi"],
                     help="config2 = headline; others are extra measurements (not the bench line)")
     ap.add_argument("--pages", type=int, default=1000, help="config5: 64 MiB pages per GPU")
     ap.add_argument("--span-len", type=int, default=4133, help="config2r: span length (stride = len + 32)")
@@ -683,7 +687,7 @@ def extra_workload(args):
         kms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
         res.update(config=cfg, kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
                    hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
-    elif args.workload in ("config5", "pagesmix"):
+    elif args.workload in ("config5", "pagesmix", "mixed41"):
         vargs, ok, victims, nbytes, cfg = (workload_config5 if args.workload == "config5" else
                                            workload_pagesmix)(args, rank, world)
         res["settle_launches"] = settle(lambda k: run_verify_steps(vargs, k, stream), args.settle_ms)

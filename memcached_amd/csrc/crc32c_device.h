@@ -105,6 +105,12 @@ constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 #endif
 // k_lines stamps (MODE 2): the epoch lane stores each fused image's CRC itself
 // (1) instead of leaving {V, pad} for k_fix (0)
+#ifndef MCRC_K1_CHUNK  // K1: each wave a contiguous range of items (1), the grid-stride order (0), or
+#define MCRC_K1_CHUNK 1  // each workgroup a contiguous range, its waves interleaved (2; A/B only)
+#endif
+#ifndef MCRC_CENSUS_FORCE  // (A/B of k_census's routing; -1 in every product build)
+#define MCRC_CENSUS_FORCE -1
+#endif
 #ifndef MCRC_ABL_COUNT  // (k_count timing ablation; 0 in every product build)
 #define MCRC_ABL_COUNT 0
 #endif

@@ -155,7 +155,30 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // divergent exit merged an un-waited path there and forced vmcnt(0),
     // which drained the prefetched step).
     uint64_t grp = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
+#if MCRC_K1_CHUNK == 2
+    // (A/B) workgroup b takes the contiguous groups [b 16 cg, (b + 1) 16 cg),
+    // its 16 waves interleaved
+    const uint64_t cg = (ngroups + gstep - 1) / gstep;
+    const uint64_t gbase = (uint64_t)blockIdx.x * waves * cg;
+    const uint64_t gend = min(gbase + waves * cg, ngroups);
+    grp = gbase + (threadIdx.x >> 6);
+    if (grp >= gend) return;
+    const uint64_t gs = waves, glast = grp + (gend - grp - 1) / gs * gs;
+#elif MCRC_K1_CHUNK
+    // wave w takes the contiguous groups [w cg, (w + 1) cg): 1.0-1.4 % faster
+    // than the grid-stride order at 1 Mi items, 0.6-3.7 % at 4 Mi, on two
+    // boxes (profiles/r04_ablations/k1_chunk_and_census_ab.txt,
+    // k1_item_order_ab.txt); a range per workgroup with its waves interleaved
+    // was 4.5 % slower
+    const uint64_t cg = (ngroups + gstep - 1) / gstep;
+    const uint64_t gend = min((grp + 1) * cg, ngroups);
+    grp *= cg;
     if (grp >= ngroups) return;
+    const uint64_t gs = 1, glast = gend - 1;
+#else
+    if (grp >= ngroups) return;
+    const uint64_t gs = gstep;
+#endif
     auto item_of = [&](uint64_t gi) { return gi * IPW + g; };
 
     Regs ra, rb;
@@ -167,7 +190,11 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // the step: left alone, the scheduler sinks them into the chains and the
     // next step waits on loads issued moments before.
     auto ld = [&](Regs &r, uint64_t gi) {
+#if MCRC_K1_CHUNK
+        const uint64_t gu = gi < gend ? gi : glast;
+#else
         const uint64_t gu = gi < ngroups ? gi : gi - gstep < ngroups ? gi - gstep : ngroups - 1;
+#endif
         const uint64_t first = gu * IPW;
         const uint8_t *wb = base + first * stride;
         const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
@@ -186,33 +213,37 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // One exit, at the bottom of each loop: a break between the halves would
     // give the loop header a second (un-waited) predecessor, and the waitcnt
     // pass would then drain every prefetched load there.
+#if MCRC_K1_CHUNK
+    const uint64_t nsteps = (gend - grp + gs - 1) / gs;
+#else
     const uint64_t nsteps = (ngroups - grp + gstep - 1) / gstep;
+#endif
     ld(ra, grp);
     uint64_t k = 0;
     for (; k + 4 <= nsteps; k += 4) {
-        ld(rb, grp + gstep);
+        ld(rb, grp + gs);
         const uint32_t va = part0(ra);
-        ld(ra, grp + 2 * gstep);
+        ld(ra, grp + 2 * gs);
         const uint32_t vb = part0(rb);
         const uint32_t vab = group_pair_level1(va, vb, lane);
-        ld(rb, grp + 3 * gstep);
+        ld(rb, grp + 3 * gs);
         const uint32_t vc = part0(ra);
-        ld(ra, grp + 4 * gstep);
+        ld(ra, grp + 4 * gs);
         const uint32_t vd = part0(rb);
         const uint32_t raw = group_reduce32_quad(vab, group_pair_level1(vc, vd, lane), lane);
-        const uint64_t item = item_of(grp + (li & 3u) * gstep);
+        const uint64_t item = item_of(grp + (li & 3u) * gs);
         if (li < 4 && item < nitems) out[item] = ~raw;
-        grp += 4 * gstep;
+        grp += 4 * gs;
     }
     for (; k + 2 <= nsteps; k += 2) {
-        ld(rb, grp + gstep);
+        ld(rb, grp + gs);
         const uint32_t va = part0(ra);
-        ld(ra, grp + 2 * gstep);
+        ld(ra, grp + 2 * gs);
         const uint32_t vb = part0(rb);
         const uint32_t raw = group_reduce32_pair(va, vb, lane);
-        const uint64_t item = item_of(li == 0 ? grp : grp + gstep);
+        const uint64_t item = item_of(li == 0 ? grp : grp + gs);
         if (li < 2 && item < nitems) out[item] = ~raw;
-        grp += 2 * gstep;
+        grp += 2 * gs;
     }
     if (nsteps & 1) {
         if (li == 0) ra.d[0][0].x ^= ~ra.cin;
@@ -2441,7 +2472,11 @@ __global__ __launch_bounds__(kCensus) void k_census(SpanArgs a, uint32_t *route)
         if (it.sane && fused) atomicAdd(&cnt, 1u);
     }
     __syncthreads();
+#if MCRC_CENSUS_FORCE >= 0  // (A/B only: every batch to K5 (1) or to the planned path (0))
+    if (threadIdx.x == 0) *route = MCRC_CENSUS_FORCE;
+#else
     if (threadIdx.x == 0) *route = 16ull * cnt >= 15ull * s ? 1u : 0u;
+#endif
 }
 
 // Fallback lists: gather the listed items' offsets / scatter their results.
