@@ -8,6 +8,12 @@
 #if defined(__x86_64__)
 #include <cpuid.h>
 #include <nmmintrin.h>
+#elif defined(__aarch64__)
+#include <arm_acle.h>
+#include <sys/auxv.h>
+#ifndef HWCAP_CRC32
+#define HWCAP_CRC32 (1ul << 7)
+#endif
 #endif
 
 namespace mcrc {
@@ -88,18 +94,31 @@ uint32_t reg_sw_big(uint32_t r, const unsigned char *p, size_t n) {
     return r;
 }
 
+// The CRC32C instruction: SSE4.2 crc32 on x86-64; on arm64 the ARMv8 CRC
+// extension's crc32cb / crc32cx (crc32c.c:285-336 uses the latter the same way).
 #if defined(__x86_64__)
+#define MCRC_HW_TARGET __attribute__((target("sse4.2")))
+MCRC_HW_TARGET inline uint64_t hw_u64(uint64_t r, uint64_t v) { return _mm_crc32_u64(r, v); }
+MCRC_HW_TARGET inline uint64_t hw_u8(uint64_t r, unsigned char b) { return _mm_crc32_u8((uint32_t)r, b); }
+#elif defined(__aarch64__)
+#define MCRC_HW_TARGET __attribute__((target("crc")))
+MCRC_HW_TARGET inline uint64_t hw_u64(uint64_t r, uint64_t v) { return __crc32cd((uint32_t)r, v); }
+MCRC_HW_TARGET inline uint64_t hw_u8(uint64_t r, unsigned char b) { return __crc32cb((uint32_t)r, b); }
+#endif
+
+#if defined(MCRC_HW_TARGET)
 // Three streams of `blk` bytes per round: the crc32 instruction has a latency of
-// three and a throughput of one, so three independent chains keep it busy.
-__attribute__((target("sse4.2"))) uint64_t three_way(uint64_t r, const unsigned char *&p, size_t &n,
-                                                     size_t blk, const uint32_t (*shift)[256]) {
+// three and a throughput of one (x86-64; arm64 cores are alike), so three
+// independent chains keep it busy.
+MCRC_HW_TARGET uint64_t three_way(uint64_t r, const unsigned char *&p, size_t &n, size_t blk,
+                                  const uint32_t (*shift)[256]) {
     while (n >= 3 * blk) {
         uint64_t a = r, b = 0, c = 0;
         const unsigned char *pa = p, *pb = p + blk, *pc = p + 2 * blk;
         for (size_t i = 0; i < blk; i += 8) {
-            a = _mm_crc32_u64(a, load64(pa + i));
-            b = _mm_crc32_u64(b, load64(pb + i));
-            c = _mm_crc32_u64(c, load64(pc + i));
+            a = hw_u64(a, load64(pa + i));
+            b = hw_u64(b, load64(pb + i));
+            c = hw_u64(c, load64(pc + i));
         }
         r = apply4(shift, apply4(shift, (uint32_t)a) ^ (uint32_t)b) ^ (uint32_t)c;
         p += 3 * blk;
@@ -108,16 +127,16 @@ __attribute__((target("sse4.2"))) uint64_t three_way(uint64_t r, const unsigned 
     return r;
 }
 
-__attribute__((target("sse4.2"))) uint32_t reg_hw(uint32_t r32, const unsigned char *p, size_t n) {
+MCRC_HW_TARGET uint32_t reg_hw(uint32_t r32, const unsigned char *p, size_t n) {
     uint64_t r = r32;
     while (n && ((uintptr_t)p & 7u)) {
-        r = _mm_crc32_u8((uint32_t)r, *p++);
+        r = hw_u8(r, *p++);
         --n;
     }
     r = three_way(r, p, n, kStreamBlock, g_shift_block);
     r = three_way(r, p, n, kSmallBlock, g_shift_small);
-    for (; n >= 8; n -= 8, p += 8) r = _mm_crc32_u64(r, load64(p));
-    while (n--) r = _mm_crc32_u8((uint32_t)r, *p++);
+    for (; n >= 8; n -= 8, p += 8) r = hw_u64(r, load64(p));
+    while (n--) r = hw_u8(r, *p++);
     return (uint32_t)r;
 }
 #endif
@@ -126,11 +145,13 @@ __attribute__((target("sse4.2"))) uint32_t reg_hw(uint32_t r32, const unsigned c
 
 void host_tables_init() { std::call_once(g_once, build_all); }
 
-bool host_has_sse42() {
+bool host_has_hw_crc() {
 #if defined(__x86_64__)
     unsigned eax, ebx, ecx, edx;
     if (!__get_cpuid(1, &eax, &ebx, &ecx, &edx)) return false;
-    return (ecx >> 20) & 1u;
+    return (ecx >> 20) & 1u;  // SSE4.2
+#elif defined(__aarch64__)
+    return (getauxval(AT_HWCAP) & HWCAP_CRC32) != 0;  // crc32c.c:266-275 probes the same
 #else
     return false;
 #endif
@@ -148,7 +169,7 @@ uint32_t crc32c_host_sw_big(uint32_t crc, const void *buf, size_t len) {
 
 uint32_t crc32c_host_hw(uint32_t crc, const void *buf, size_t len) {
     host_tables_init();
-#if defined(__x86_64__)
+#if defined(MCRC_HW_TARGET)
     return ~reg_hw(~crc, static_cast<const unsigned char *>(buf), len);
 #else
     return ~reg_sw(~crc, static_cast<const unsigned char *>(buf), len);

@@ -40,7 +40,7 @@ crc_func crc32c = nullptr;
 
 void crc32c_init(void) {
     mcrc::host_tables_init();
-    crc32c = mcrc::host_has_sse42() ? mcrc::crc32c_host_hw : mcrc::crc32c_host_sw;
+    crc32c = mcrc::host_has_hw_crc() ? mcrc::crc32c_host_hw : mcrc::crc32c_host_sw;
 }
 
 uint32_t crc32c_sw(uint32_t crc, void const *buf, size_t len) { return mcrc::crc32c_host_sw(crc, buf, len); }
