@@ -1098,15 +1098,21 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
 // whose span is whole (span_corr's first case: the thread's alone).  A whole
 // span's chain used to run in its lane while the lanes without one idled
 // (one whole span in seven on the mixed pages: 0.11 of k_count's 0.21 ms);
-// now the wave cuts the pieces of all its whole spans into 64-B chunks and
-// every lane takes one: r_c = raw of its <= 4 pieces, shifted past the rest of
+// now the wave cuts the pieces of all its whole spans into 128-B chunks and
+// every lane takes one: r_c = raw of its <= 8 pieces, shifted past the rest of
 // its span (M_{Ea - end}, x^(8 n) from the xpow table), XORed into the span's
 // slot (LDS, wave-private).  tests/test_count_whole_model.py restates it.
 constexpr uint32_t kCountThreads = 256;
+#ifndef MCRC_WHOLE_PIECES
+#define MCRC_WHOLE_PIECES 8
+#endif
+// (128-B chunks: half the x^(8n) multiplies of 64-B ones, mixed pages -0.6 %;
+// 256-B chunks' longer lane chains were slower: k_count_chunk_size_ab.txt)
+constexpr uint32_t kWholePieces = MCRC_WHOLE_PIECES, kWholeChunk = 16 * kWholePieces;  // pieces / bytes per chunk
 __device__ __forceinline__ uint32_t whole_chunks(gbyte *gb, bool whole, uint64_t ph, uint64_t ea, const Tab8 &t,
                                                  const uint32_t *xp, uint32_t *slot) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nch = whole ? (uint32_t)((ea - ph + 63u) >> 6) : 0u;
+    const uint32_t nch = whole ? (uint32_t)((ea - ph + kWholeChunk - 1u) / kWholeChunk) : 0u;
     uint32_t inc = nch;  // inclusive chunk count over the wave
 #pragma unroll
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -1128,14 +1134,14 @@ __device__ __forceinline__ uint32_t whole_chunks(gbyte *gb, bool whole, uint64_t
         const uint64_t sea = (uint32_t)__shfl((int)(uint32_t)ea, (int)s, 64) |
                              ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ea >> 32), (int)s, 64) << 32);
         const bool act = q < total;
-        const uint64_t c0 = sph + 64ull * c;
-        const uint32_t np = act ? (uint32_t)min((sea - c0) >> 4, (uint64_t)4) : 0u;
-        Piece pc[4];
+        const uint64_t c0 = sph + (uint64_t)kWholeChunk * c;
+        const uint32_t np = act ? (uint32_t)min((sea - c0) >> 4, (uint64_t)kWholePieces) : 0u;
+        Piece pc[kWholePieces];
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) pc[k] = k < np ? ld_piece(gb + c0 + 16u * k) : Piece{0, 0};
+        for (uint32_t k = 0; k < kWholePieces; ++k) pc[k] = k < np ? ld_piece(gb + c0 + 16u * k) : Piece{0, 0};
         uint32_t r = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
+        for (uint32_t k = 0; k < kWholePieces; ++k) {
             const uint32_t nx = t.piece(r, pc[k]);
             r = k < np ? nx : r;
         }

@@ -39,11 +39,11 @@ def is_whole(p, length):
     return length > 0 and drop and g1o == length + tail_pad(p, length)
 
 
-def chunks_R(buf, ph, ea):
-    """R as the wave forms it from 64-B chunks."""
+def chunks_R(buf, ph, ea, chunk=CHUNK):
+    """R as the wave forms it from chunk-byte chunks (kWholeChunk)."""
     R = 0
-    for c0 in range(ph, ea, CHUNK):
-        np_ = min(4, (ea - c0) // 16)
+    for c0 in range(ph, ea, chunk):
+        np_ = min(chunk // 16, (ea - c0) // 16)
         r = 0
         for k in range(np_):
             r = reg(r, buf[c0 + 16 * k:c0 + 16 * k + 16])
@@ -93,6 +93,8 @@ def test_whole_span_chunks_give_the_thread_chain(seed):
         ph, ea = p - (p & 15), p + length + t
         R = chunks_R(buf, ph, ea)
         assert R == raw(buf[ph:ea])
+        for chunk in (32, 128, 256):  # (kWholeChunk = 16 * MCRC_WHOLE_PIECES)
+            assert chunks_R(buf, ph, ea, chunk) == R
         f = reg(~c & M32, buf[p:p + length])
         assert R ^ z_pieces(buf, p, length, c) == zeros(f, t)  # = span_corr's M_t(f)
         assert ~f & M32 == oracle.crc32c(c, buf[p:p + length])
