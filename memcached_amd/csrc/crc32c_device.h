@@ -108,6 +108,12 @@ constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 #ifndef MCRC_K1_CHUNK  // K1: each wave a contiguous range of items (1), the grid-stride order (0), or
 #define MCRC_K1_CHUNK 1  // each workgroup a contiguous range, its waves interleaved (2; A/B only)
 #endif
+#ifndef MCRC_FIX_NT  // k_fix's stamps as non-temporal stores (1) or plain ones (0, A/B)
+#define MCRC_FIX_NT 1
+#endif
+#ifndef MCRC_ABL_NOFIX  // (ablation, wrong results: no k_fix pass; 0 in every product build)
+#define MCRC_ABL_NOFIX 0
+#endif
 #ifndef MCRC_CENSUS_FORCE  // (A/B of k_census's routing; -1 in every product build)
 #define MCRC_CENSUS_FORCE -1
 #endif

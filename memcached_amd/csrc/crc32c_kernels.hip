@@ -2444,7 +2444,16 @@ __global__ void k_fix(SpanArgs a, const uint2 *rt, const uint32_t *route) {
         if (r.y & kRtFused) {
             const uint32_t crc = ~mulmodp_dev(r.x, a.xpow[kXpowInv + (r.y & 15u)]);
             uint8_t *p = const_cast<uint8_t *>(a.base) + a.offsets[i] + 32;
+#if MCRC_FIX_NT
+            // non-temporal: plain stores left 16 M dirty 32-B sectors in the
+            // caches, written back while the next batch streamed (its
+            // k_lines<2> 0.11 ms slower per 300 pages); so the write-backs
+            // happen here (k_fix 0.17 -> 0.25 ms), stamp -1.2 % in all
+            // (profiles/r04_ablations/k_fix_nontemporal_ab.txt)
+            for (int b = 0; b < 4; ++b) __builtin_nontemporal_store((uint8_t)(crc >> (8 * b)), p - 4 + b);
+#else
             __builtin_memcpy(p - 4, &crc, 4);
+#endif
             if (a.ok) a.ok[i] = 1;
         }
     }
