@@ -103,25 +103,11 @@ constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 #ifndef MCRC_K5_CHUNK
 #define MCRC_K5_CHUNK 1
 #endif
-// k_lines stamps (MODE 2): the epoch lane stores each fused image's CRC itself
-// (1) instead of leaving {V, pad} for k_fix (0)
-#ifndef MCRC_K1_CHUNK  // K1: each wave a contiguous range of items (1), the grid-stride order (0), or
-#define MCRC_K1_CHUNK 1  // each workgroup a contiguous range, its waves interleaved (2; A/B only)
+#ifndef MCRC_K1_CHUNK  // K1: each wave a contiguous range of items (1) or the grid-stride order (0)
+#define MCRC_K1_CHUNK 1
 #endif
 #ifndef MCRC_FIX_NT  // k_fix's stamps as non-temporal stores (1) or plain ones (0, A/B)
 #define MCRC_FIX_NT 1
-#endif
-#ifndef MCRC_ABL_NOFIX  // (ablation, wrong results: no k_fix pass; 0 in every product build)
-#define MCRC_ABL_NOFIX 0
-#endif
-#ifndef MCRC_CENSUS_FORCE  // (A/B of k_census's routing; -1 in every product build)
-#define MCRC_CENSUS_FORCE -1
-#endif
-#ifndef MCRC_ABL_COUNT  // (k_count timing ablation; 0 in every product build)
-#define MCRC_ABL_COUNT 0
-#endif
-#ifndef MCRC_K5_STAMP
-#define MCRC_K5_STAMP 0
 #endif
 // Nibble form of the shifted tables (MCRC_NIB): set s (row chain s, shift
 // M_{(3-s)*1024}) holds 8 tables of 16 entries, table 2k + h for nibble h of

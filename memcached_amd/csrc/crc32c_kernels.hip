@@ -98,25 +98,6 @@ __device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &
             }
         }
     }
-#if defined(MCRC_K1_SENS)
-    // sensitivity ablations (timing only): 1 = +64 VALU per lane-step
-    // (dependent v_xor), 2 = +32 conflict-free LDS reads (+16 v_bitop3)
-    uint32_t z = x[0];
-    if constexpr (MCRC_K1_SENS == 1) {
-#pragma unroll
-        for (int k = 0; k < 64; ++k) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z) : "v"(x[k & 3]));
-    } else {
-#pragma unroll
-        for (int k = 0; k < 32; k += 2) {
-            const uint32_t a = lds_ld(kAux4Bytes + 256u * (uint32_t)k + c.lane4);
-            const uint32_t b = lds_ld(kAux4Bytes + 256u * (uint32_t)k + 256u + c.lane4);
-            z = xor3(z, a, b);
-        }
-        asm volatile("" : "+v"(z));
-    }
-    x[0] ^= z & 0u;
-    asm volatile("" :: "v"(z));
-#endif
     return xor3(x[0], x[1], x[2]) ^ x[3];
 }
 
@@ -155,16 +136,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // divergent exit merged an un-waited path there and forced vmcnt(0),
     // which drained the prefetched step).
     uint64_t grp = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
-#if MCRC_K1_CHUNK == 2
-    // (A/B) workgroup b takes the contiguous groups [b 16 cg, (b + 1) 16 cg),
-    // its 16 waves interleaved
-    const uint64_t cg = (ngroups + gstep - 1) / gstep;
-    const uint64_t gbase = (uint64_t)blockIdx.x * waves * cg;
-    const uint64_t gend = min(gbase + waves * cg, ngroups);
-    grp = gbase + (threadIdx.x >> 6);
-    if (grp >= gend) return;
-    const uint64_t gs = waves, glast = grp + (gend - grp - 1) / gs * gs;
-#elif MCRC_K1_CHUNK
+#if MCRC_K1_CHUNK
     // wave w takes the contiguous groups [w cg, (w + 1) cg): 1.0-1.4 % faster
     // than the grid-stride order at 1 Mi items, 0.6-3.7 % at 4 Mi, on two
     // boxes (profiles/r04_ablations/k1_chunk_and_census_ab.txt,
@@ -481,10 +453,7 @@ __device__ __forceinline__ Piece clear_below(Piece v, uint32_t k) {
 // (leading zeros leave a zero register unchanged), so
 //   r' = M_m(r) ^ raw16(the m bytes at the top).
 // Every load is an aligned piece holding a byte of [p, p + n).
-#ifndef MCRC_ADV_UNROLL
-#define MCRC_ADV_UNROLL 4
-#endif
-constexpr int kAdvUnroll = MCRC_ADV_UNROLL;
+constexpr int kAdvUnroll = 4;  // (8 and 16 measured slower: profiles/r04_ablations/k_count_unroll_ab.txt)
 __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, uint32_t n, const Tab8 &t) {
     if (n == 0) return r;
     const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
@@ -1079,12 +1048,6 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
     const uint64_t off = (uint64_t)(it.p - a.base);
     uint32_t z = 0;
     if (it.sane) {
-#if MCRC_ABL_COUNT  // (ablation, wrong results: 1 = whole spans' chains skipped, 2 = every chain skipped)
-        const SpanHead hh = span_head(it.p, it.len);
-        const bool wh = hh.drop && hh.g1o == (uint64_t)it.len + tail_pad(it.p, it.len);
-        if (MCRC_ABL_COUNT == 2 || wh) z = it.len;
-        else
-#endif
         // (a whole span's R from the wave, whole_chunks: z = R ^ Z of its pieces)
         z = whole ? rwhole ^ span_corr_pieces(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow)
                   : span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow);
@@ -1103,12 +1066,9 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
 // its span (M_{Ea - end}, x^(8 n) from the xpow table), XORed into the span's
 // slot (LDS, wave-private).  tests/test_count_whole_model.py restates it.
 constexpr uint32_t kCountThreads = 256;
-#ifndef MCRC_WHOLE_PIECES
-#define MCRC_WHOLE_PIECES 8
-#endif
 // (128-B chunks: half the x^(8n) multiplies of 64-B ones, mixed pages -0.6 %;
 // 256-B chunks' longer lane chains were slower: k_count_chunk_size_ab.txt)
-constexpr uint32_t kWholePieces = MCRC_WHOLE_PIECES, kWholeChunk = 16 * kWholePieces;  // pieces / bytes per chunk
+constexpr uint32_t kWholePieces = 8, kWholeChunk = 16 * kWholePieces;  // pieces / bytes per chunk
 __device__ __forceinline__ uint32_t whole_chunks(gbyte *gb, bool whole, uint64_t ph, uint64_t ea, const Tab8 &t,
                                                  const uint32_t *xp, uint32_t *slot) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -1307,10 +1267,7 @@ __global__ __launch_bounds__(1024) void k_scan32(const uint32_t *in, uint64_t m,
 // as one unit each by a second pass; *nvalid = records written before the
 // first such span (zeroed by the caller: none fit).  Spans of more than kExpandInline segments are listed in `big`
 // and expanded by k_expand_big, one workgroup per span.
-#ifndef MCRC_EXPAND_INLINE
-#define MCRC_EXPAND_INLINE 32
-#endif
-constexpr uint32_t kExpandInline = MCRC_EXPAND_INLINE;
+constexpr uint32_t kExpandInline = 32;
 // A device-counted list (K5's fallback: a few hundred images whose length
 // bits flipped) lands in one or two tiles, so its long spans go to
 // k_expand_big sooner: k_expand 0.031 -> 0.012 ms per 300-page verify; at 8
@@ -1941,9 +1898,6 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
     auto prep_pieces = [&]() {
 #pragma unroll
         for (uint32_t k = 0; k < kFragPieces; ++k) pc[k] = ld16(k < p_np16 ? gb + p_pho + 16 * k : gz);
-#if defined(MCRC_K5_ABL) && (MCRC_K5_ABL & 1)  // ablation: no fragment reads (results wrong)
-        for (uint32_t k = 0; k < kFragPieces; ++k) pc[k] = ld16(gz);
-#endif
     };
     // r = register from ~c over [p, G): the pieces of [floor16(p), G), bytes
     // below p cleared and ~c injected at p (head_dword); C = M_4096(r)
@@ -1968,24 +1922,10 @@ __global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restr
     // Loads of step s (< ns, else a repeat of the epoch's last step, whose
     // result is not used) into b: its block and its status.
     auto ld = [&](ItemBuf &b, uint32_t s, uint32_t ns) {
-#if defined(MCRC_K5_RL)
-        // (the step is wave-uniform: the two groups' descriptors are lanes
-        // 2s and 2s + 1, read as scalars, no ds_bpermute)
-        const int s2 = (int)__builtin_amdgcn_readfirstlane(2 * min(s, ns - 1));
-        const uint32_t lo0 = __builtin_amdgcn_readlane(eglo, s2), lo1 = __builtin_amdgcn_readlane(eglo, s2 + 1);
-        const uint32_t hi0 = __builtin_amdgcn_readlane(eghi, s2), hi1 = __builtin_amdgcn_readlane(eghi, s2 + 1);
-        const uint32_t st0 = __builtin_amdgcn_readlane(est, s2), st1 = __builtin_amdgcn_readlane(est, s2 + 1);
-        const uint64_t lo = g ? lo1 : lo0, hi = g ? hi1 : hi0;
-        b.st = g ? st1 : st0;
-#else
         const int src = (int)(2 * min(s, ns - 1) + g);
         const uint64_t lo = (uint32_t)__shfl((int)eglo, src, 64), hi = (uint32_t)__shfl((int)eghi, src, 64);
         b.st = (uint32_t)__shfl((int)est, src, 64);
-#endif
         gbyte *blk = (b.st & kStFused) ? gb + (lo | (hi << 32)) : gz;
-#if defined(MCRC_K5_ABL) && (MCRC_K5_ABL & 2)  // ablation: blocks on 128-B lines (results wrong)
-        blk = (gbyte *)((uintptr_t)blk & ~(uintptr_t)127);
-#endif
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -2340,16 +2280,7 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
                     nb += !good;
                 }
             } else {
-#if MCRC_K5_STAMP && !MCRC_K5_ITEMS
-                if (fused) {
-                    const uint32_t crc = ~mulmodp_dev(v, io.xk[0u - pad - (uint32_t)kXkLo]);
-                    uint8_t *const at = const_cast<uint8_t *>(a.base) + p_pho + p_kh - 4;  // exptime
-                    __builtin_memcpy(at, &crc, 4);
-                    if (a.ok) a.ok[item] = 1;
-                }
-#else
                 io.rt[item] = fused ? make_uint2(v, pad | kRtFused) : make_uint2(0u, 0u);
-#endif
                 if (!sane) {
                     if (a.ok) a.ok[item] = 0;
                     ++nb;
@@ -2487,11 +2418,7 @@ __global__ __launch_bounds__(kCensus) void k_census(SpanArgs a, uint32_t *route)
         if (it.sane && fused) atomicAdd(&cnt, 1u);
     }
     __syncthreads();
-#if MCRC_CENSUS_FORCE >= 0  // (A/B only: every batch to K5 (1) or to the planned path (0))
-    if (threadIdx.x == 0) *route = MCRC_CENSUS_FORCE;
-#else
     if (threadIdx.x == 0) *route = 16ull * cnt >= 15ull * s ? 1u : 0u;
-#endif
 }
 
 // Fallback lists: gather the listed items' offsets / scatter their results.

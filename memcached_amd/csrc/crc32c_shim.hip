@@ -609,7 +609,7 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     hipLaunchKernelGGL(mcrc_dev::k_census<MODE>, dim3(1), dim3(mcrc_dev::kCensus), 0, st, a, d.route);
     launch_k5<MODE, true>(d, a, io, st);
     const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 1024);
-    if (MODE == 2 && !(MCRC_K5_STAMP && !MCRC_K5_ITEMS) && !MCRC_ABL_NOFIX)
+    if (MODE == 2)
         hipLaunchKernelGGL(mcrc_dev::k_fix, dim3(g), dim3(256), 0, st, a, (const uint2 *)io.rt,
                            (const uint32_t *)d.route);
     hipLaunchKernelGGL(mcrc_dev::k_gather_offs, dim3(g), dim3(256), 0, st, a.offsets, (const uint32_t *)io.fb,
