@@ -106,6 +106,9 @@ constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 #ifndef MCRC_K1_CHUNK  // K1: each wave a contiguous range of items (1) or the grid-stride order (0)
 #define MCRC_K1_CHUNK 1
 #endif
+#ifndef MCRC_K1_PERM  // K1's ranges dealt in a scrambled wave order (1) or in wave order (0)
+#define MCRC_K1_PERM 1
+#endif
 #ifndef MCRC_FIX_NT  // k_fix's stamps as non-temporal stores (1) or plain ones (0, A/B)
 #define MCRC_FIX_NT 1
 #endif

@@ -136,6 +136,14 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // divergent exit merged an un-waited path there and forced vmcnt(0),
     // which drained the prefetched step).
     uint64_t grp = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
+#if MCRC_K1_CHUNK && MCRC_K1_PERM
+    // the ranges dealt to the waves in a scrambled order: wave w takes range
+    // (w * 65521) mod W (65521 is prime: a bijection unless it divides W), so
+    // a CU's 16 waves stream ranges far apart rather than 16 neighbouring
+    // MiB: -0.6 % at 1 and 4 Mi items in every round
+    // (profiles/r04_ablations/k1_range_order_ab.txt)
+    if (gstep % 65521u) grp = (grp * 65521u) % gstep;
+#endif
 #if MCRC_K1_CHUNK
     // wave w takes the contiguous groups [w cg, (w + 1) cg): 1.0-1.4 % faster
     // than the grid-stride order at 1 Mi items, 0.6-3.7 % at 4 Mi, on two
