@@ -808,6 +808,40 @@ def extra_workload(args):
         pin64 = torch.from_numpy(host).pin_memory()
         hs_pin = _lib.Spans(pin64.data_ptr(), host.size, hoffs.ctypes.data, 0, None, 4133, None, hout.ctypes.data, 64)
         host64_pin_us = per_call(lambda: _lib.check(_lib.lib.crc32c_batch(ctypes.byref(hs_pin), 0, None)), 200)
+        # host cost of enqueueing one asynchronous device batch (K1, 16 Ki x
+        # 4 KiB of the page buffer), one thread, then 8 threads at once on
+        # their own streams (the per-call device lookup takes no process-wide
+        # lock: DESIGN.md section 6); ctypes releases the GIL during the call
+        import threading
+        n1 = 16384
+        k1out = torch.empty(n1 * 8, dtype=torch.int32, device="cuda")
+
+        def enqueue_loop(t, reps, st, times):
+            sp1 = _lib.Spans(base, n1 * 4096, None, 4096, None, 4096, None, k1out.data_ptr() + 4 * n1 * t, n1)
+            sp_ptr = ctypes.c_void_p(st.cuda_stream)
+            flags = _lib.CRC32C_DEVICE | _lib.CRC32C_ASYNC
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp1), flags, sp_ptr))
+            times[t] = (time.perf_counter() - t0) / reps * 1e6
+
+        streams = [torch.cuda.Stream() for _ in range(8)]
+        enq = {}
+        for nth in (1, 8):
+            times = [0.0] * nth
+            enqueue_loop(0, 10, streams[0], [0.0])  # (warm)
+            torch.cuda.synchronize()
+            ths = [threading.Thread(target=enqueue_loop, args=(t, 100, streams[t], times)) for t in range(nth)]
+            w0 = time.perf_counter()
+            for th in ths:
+                th.start()
+            for th in ths:
+                th.join()
+            wall = time.perf_counter() - w0
+            torch.cuda.synchronize()
+            enq[nth] = (max(times), wall / (100 * nth) * 1e6)
+        res.update(enqueue_async_us_1thread=round(enq[1][0], 2), enqueue_async_us_8threads=round(enq[8][0], 2),
+                   enqueue_async_8threads_wall_us_per_call=round(enq[8][1], 2))
         res.update(config={"workload": "per-call latency, synchronous calls, one thread: stamp one 4 MiB wbuf of "
                                        "1007 images (device; host page-locked; host pageable), verify an IO batch "
                                        "of 64 images (device; host page-locked), CRC 64 x 4133-B spans in host "

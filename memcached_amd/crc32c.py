@@ -77,14 +77,20 @@ def _check_dev(t, name, n, dtypes):
 
 
 def batch(buf, offsets=None, stride: int = 0, lens=None, length: int = 0, crc_in=None, out=None,
-          stream=None, asynchronous: bool = False):
+          stream=None, asynchronous: bool = False, aligned16=None):
     """Batched CRC-32C of spans of ``buf``.
 
     Span i = buf[off_i : off_i + len_i] with off_i = offsets[i] (or i*stride)
     and len_i = lens[i] (or ``length``).  Host numpy inputs take the pinned
     staging path; torch device tensors run in place on the current stream.
-    Returns ``out`` (uint32, one CRC per span).
+    Returns ``out`` (uint32, one CRC per span).  ``aligned16`` is accepted and
+    ignored, as the C ABI ignores its retired flag bit 0x4 (the kernels test
+    alignment themselves).
     """
+    if aligned16 is not None:
+        import warnings
+        warnings.warn("batch(aligned16=...) is ignored (alignment is detected per batch)", DeprecationWarning,
+                      stacklevel=2)
     dev = _is_torch(buf) and buf.is_cuda
     if offsets is not None:
         n = len(offsets)

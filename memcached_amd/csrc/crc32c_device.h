@@ -90,78 +90,12 @@ __device__ __forceinline__ uint32_t step4_next(uint32_t x, uint32_t w_next, cons
 constexpr uint32_t kAuxShift0 = 156, kAuxShift1 = 24, kAuxShift2 = 20;
 constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 
-#ifndef MCRC_NIB
-#define MCRC_NIB 0
-#endif
-// MCRC_K5_ITEMS=1: K5 as k_items (round 3, 16-B-anchored blocks) instead of
-// the line-anchored k_lines (A/B builds)
-#ifndef MCRC_K5_ITEMS
-#define MCRC_K5_ITEMS 0
-#endif
-// k_lines: a contiguous chunk of images per wave with staggered runs (0: the
-// round-robin runs of the first k_lines, kept for A/B)
-#ifndef MCRC_K5_CHUNK
-#define MCRC_K5_CHUNK 1
-#endif
-#ifndef MCRC_K1_CHUNK  // K1: each wave a contiguous range of items (1) or the grid-stride order (0)
-#define MCRC_K1_CHUNK 1
-#endif
-#ifndef MCRC_K1_PERM  // K1's ranges dealt in a scrambled wave order (1) or in wave order (0)
-#define MCRC_K1_PERM 1
-#endif
-#ifndef MCRC_FIX_NT  // k_fix's stamps as non-temporal stores (1) or plain ones (0, A/B)
-#define MCRC_FIX_NT 1
-#endif
-// Nibble form of the shifted tables (MCRC_NIB): set s (row chain s, shift
-// M_{(3-s)*1024}) holds 8 tables of 16 entries, table 2k + h for nibble h of
-// byte k, at kNibShiftBytes + 512 s + 64 (2k + h).  A 16-entry table spans 16
-// banks with one entry per bank, so any 32 lanes read it conflict-free (the
-// byte tables, 8 entries per bank, cost ~2.2 extra LDS cycles per 32 lanes).
-constexpr uint32_t kNibShiftBytes = 20 * 1024;
-constexpr uint32_t nib_set(uint32_t t0) { return t0 == kAuxShift0 ? 0u : t0 == kAuxShift1 ? 1u : 2u; }
-
-// MCRC_NIB == 2: level 0 of the lane tree folded into the chains as well.
-// Every row's last step reads nibble tables: row r of an even lane ends with
-// M_{(3-r)*1024 + 32} (its odd neighbour's 32 bytes follow), of an odd lane
-// with M_{(3-r)*1024}, so level 0 is a plain XOR of the two lanes.  Set
-// (r, parity p): table k (nibble k) at kNibShiftBytes + 1024 r + 128 k + 64 p
-// -- even lanes' tables in banks 0-15, odd lanes' in 16-31: still one entry
-// per bank per instruction.
-__device__ __forceinline__ uint32_t step4_last_nib2(uint32_t x, uint32_t r, uint32_t par64x4) {
-    uint32_t lo = __builtin_amdgcn_alignbit(x, x, 30), hi = __builtin_amdgcn_alignbit(x, x, 2);
-    asm volatile("" : "+v"(lo), "+v"(hi));
-    // nibble * 4 in bits 2..5 of every byte, the lane's parity in bit 6
-    lo = (lo & 0x3c3c3c3cu) | par64x4;
-    hi = (hi & 0x3c3c3c3cu) | par64x4;
-    const uint32_t b = kNibShiftBytes + 1024u * r;
-    return xor3(xor3(lds_ld(b + (lo & 0xffu)), lds_ld(b + 128 + (hi & 0xffu)), lds_ld(b + 256 + ((lo >> 8) & 0xffu))),
-                xor3(lds_ld(b + 384 + ((hi >> 8) & 0xffu)), lds_ld(b + 512 + ((lo >> 16) & 0xffu)),
-                     lds_ld(b + 640 + ((hi >> 16) & 0xffu))),
-                lds_ld(b + 768 + (lo >> 24))) ^
-           lds_ld(b + 896 + (hi >> 24));
-}
-
 // Last slice-by-4 step of a row chain through the shifted tables t0..t0+3:
 // returns M_shift(T3[x0] ^ T2[x1] ^ T1[x2] ^ T0[x3]).
 __device__ __forceinline__ uint32_t step4_last_shifted(uint32_t x, uint32_t t0) {
-#if MCRC_NIB
-    // rotl 2 puts the low nibble of byte k at bits 2..5 of byte k, rotr 2 the
-    // high nibble: each address is one byte of a rotation masked to 0x3c
-    uint32_t lo = __builtin_amdgcn_alignbit(x, x, 30), hi = __builtin_amdgcn_alignbit(x, x, 2);
-    // (opaque to the optimizer: it would fold the rotations into two shifts
-    // per nibble; kept, each address is one SDWA byte-select AND)
-    asm volatile("" : "+v"(lo), "+v"(hi));
-    const uint32_t b = kNibShiftBytes + 512u * nib_set(t0);
-    return xor3(xor3(lds_ld(b + (lo & 0x3cu)), lds_ld(b + 64 + (hi & 0x3cu)), lds_ld(b + 128 + ((lo >> 8) & 0x3cu))),
-                xor3(lds_ld(b + 192 + ((hi >> 8) & 0x3cu)), lds_ld(b + 256 + ((lo >> 16) & 0x3cu)),
-                     lds_ld(b + 320 + ((hi >> 16) & 0x3cu))),
-                lds_ld(b + 384 + ((lo >> 24) & 0x3cu))) ^
-           lds_ld(b + 448 + ((hi >> 24) & 0x3cu));
-#else
     return xor3(Step<4>::aux(t0, x & 0xffu), Step<4>::aux(t0 + 1, (x >> 8) & 0xffu),
                 Step<4>::aux(t0 + 2, (x >> 16) & 0xffu)) ^
            Step<4>::aux(t0 + 3, x >> 24);
-#endif
 }
 
 // Apply the zeros operator stored in aux tables t0..t0+3.
@@ -188,11 +122,6 @@ template <int K = 0>
 __device__ __forceinline__ uint32_t group_reduce32_dpp(uint32_t v, uint32_t lane) {
     if constexpr (K == 5) {
         return v;
-#if MCRC_NIB == 2
-    } else if constexpr (K == 0) {
-        const uint32_t x = lane_down<0>(v);  // (M_32 is in the even lanes' last steps)
-        return group_reduce32_dpp<1>((lane & 1u) == 0u ? v ^ x : v, lane);
-#endif
     } else {
         const uint32_t x = lane_down<K>(v);
         if ((lane & ((2u << K) - 1u)) == 0) v = xor3(Step<4>::aux(kAuxTree + 4 * K, v & 0xffu) ^ x,
@@ -207,9 +136,6 @@ __device__ __forceinline__ uint32_t group_reduce32_dpp(uint32_t v, uint32_t lane
 template <int K>
 __device__ __forceinline__ uint32_t reduce_level(uint32_t v, bool on) {
     const uint32_t x = lane_down<K>(v);
-#if MCRC_NIB == 2
-    if constexpr (K == 0) return on ? v ^ x : v;  // (M_32 is in the even lanes' last steps)
-#endif
     if (on) v = xor3(Step<4>::aux(kAuxTree + 4 * K, v & 0xffu) ^ x, Step<4>::aux(kAuxTree + 4 * K + 1, (v >> 8) & 0xffu),
                      Step<4>::aux(kAuxTree + 4 * K + 2, (v >> 16) & 0xffu)) ^
                 Step<4>::aux(kAuxTree + 4 * K + 3, v >> 24);

@@ -198,31 +198,6 @@ inline void build_lds_image_k1(uint32_t *img, uint32_t chunk) {
         for (int j = 0; j < 4; ++j)
             for (int b = 0; b < 256; ++b) img[(slot[r] + j) * 256 + b] = m.apply(t[3 - j][b]);
     }
-#if MCRC_NIB == 2
-    // nibble sets with level 0 folded in (crc32c_device.h step4_last_nib2):
-    // set (r, p) = M_{(3-r)*32*chunk + (p ? 0 : chunk)} o T_{3-k}, table k at
-    // + 1024 r + 128 k' + 64 p for nibble k' = 2k + h
-    for (int r = 0; r < 4; ++r)
-        for (int p = 0; p < 2; ++p) {
-            const Gf2Op m = Gf2Op::zeros((uint64_t)(3 - r) * 32 * chunk + (p ? 0 : chunk));
-            for (int k = 0; k < 4; ++k)
-                for (int h = 0; h < 2; ++h)
-                    for (int n = 0; n < 16; ++n)
-                        img[(20 * 1024 + 1024 * r + 128 * (2 * k + h) + 64 * p) / 4 + n] =
-                            m.apply(t[3 - k][n << (4 * h)]);
-        }
-#elif MCRC_NIB
-    // nibble form (crc32c_device.h kNibShiftBytes), over the byte tables of
-    // S_2: table 2k + h of set r, entry n = S_r[k][n << 4h] (a byte table is
-    // linear in the byte's bits)
-    for (int r = 0; r < 3; ++r) {
-        const Gf2Op m = Gf2Op::zeros((uint64_t)(3 - r) * 32 * chunk);
-        for (int k = 0; k < 4; ++k)
-            for (int h = 0; h < 2; ++h)
-                for (int n = 0; n < 16; ++n)
-                    img[(20 * 1024 + 512 * r + 64 * (2 * k + h)) / 4 + n] = m.apply(t[3 - k][n << (4 * h)]);
-    }
-#endif
 }
 
 // Span image (160 KiB): the K1 image with aux tables 16..19 (tree level 4,

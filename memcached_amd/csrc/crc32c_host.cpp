@@ -97,20 +97,25 @@ uint32_t reg_sw_big(uint32_t r, const unsigned char *p, size_t n) {
 // The CRC32C instruction: SSE4.2 crc32 on x86-64; on arm64 the ARMv8 CRC
 // extension's crc32cb / crc32cx (crc32c.c:285-336 uses the latter the same way).
 #if defined(__x86_64__)
-#define MCRC_HW_TARGET __attribute__((target("sse4.2")))
-MCRC_HW_TARGET inline uint64_t hw_u64(uint64_t r, uint64_t v) { return _mm_crc32_u64(r, v); }
-MCRC_HW_TARGET inline uint64_t hw_u8(uint64_t r, unsigned char b) { return _mm_crc32_u8((uint32_t)r, b); }
+#define HOST_CRC_TARGET __attribute__((target("sse4.2")))
+HOST_CRC_TARGET inline uint64_t hw_u64(uint64_t r, uint64_t v) { return _mm_crc32_u64(r, v); }
+HOST_CRC_TARGET inline uint64_t hw_u8(uint64_t r, unsigned char b) { return _mm_crc32_u8((uint32_t)r, b); }
 #elif defined(__aarch64__)
-#define MCRC_HW_TARGET __attribute__((target("crc")))
-MCRC_HW_TARGET inline uint64_t hw_u64(uint64_t r, uint64_t v) { return __crc32cd((uint32_t)r, v); }
-MCRC_HW_TARGET inline uint64_t hw_u8(uint64_t r, unsigned char b) { return __crc32cb((uint32_t)r, b); }
+// (GCC spells the extension "+crc", clang "crc")
+#if defined(__clang__)
+#define HOST_CRC_TARGET __attribute__((target("crc")))
+#else
+#define HOST_CRC_TARGET __attribute__((target("+crc")))
+#endif
+HOST_CRC_TARGET inline uint64_t hw_u64(uint64_t r, uint64_t v) { return __crc32cd((uint32_t)r, v); }
+HOST_CRC_TARGET inline uint64_t hw_u8(uint64_t r, unsigned char b) { return __crc32cb((uint32_t)r, b); }
 #endif
 
-#if defined(MCRC_HW_TARGET)
+#if defined(HOST_CRC_TARGET)
 // Three streams of `blk` bytes per round: the crc32 instruction has a latency of
 // three and a throughput of one (x86-64; arm64 cores are alike), so three
 // independent chains keep it busy.
-MCRC_HW_TARGET uint64_t three_way(uint64_t r, const unsigned char *&p, size_t &n, size_t blk,
+HOST_CRC_TARGET uint64_t three_way(uint64_t r, const unsigned char *&p, size_t &n, size_t blk,
                                   const uint32_t (*shift)[256]) {
     while (n >= 3 * blk) {
         uint64_t a = r, b = 0, c = 0;
@@ -127,7 +132,7 @@ MCRC_HW_TARGET uint64_t three_way(uint64_t r, const unsigned char *&p, size_t &n
     return r;
 }
 
-MCRC_HW_TARGET uint32_t reg_hw(uint32_t r32, const unsigned char *p, size_t n) {
+HOST_CRC_TARGET uint32_t reg_hw(uint32_t r32, const unsigned char *p, size_t n) {
     uint64_t r = r32;
     while (n && ((uintptr_t)p & 7u)) {
         r = hw_u8(r, *p++);
@@ -169,7 +174,7 @@ uint32_t crc32c_host_sw_big(uint32_t crc, const void *buf, size_t len) {
 
 uint32_t crc32c_host_hw(uint32_t crc, const void *buf, size_t len) {
     host_tables_init();
-#if defined(MCRC_HW_TARGET)
+#if defined(HOST_CRC_TARGET)
     return ~reg_hw(~crc, static_cast<const unsigned char *>(buf), len);
 #else
     return ~reg_sw(~crc, static_cast<const unsigned char *>(buf), len);

@@ -29,7 +29,7 @@ namespace mcrc_dev {
 // 16-B load of item bytes.  (Non-temporal loads measured no better for K1 and
 // 5-11 % worse for the span kernels.)
 __device__ __forceinline__ uint4 ld16(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
-// Global-memory byte and piece pointers.  k_items keeps its addresses in
+// Global-memory byte and piece pointers.  k_lines keeps its addresses in
 // these: derived from the kernel arguments through generic pointers, they
 // lost their address space to an optimizer freeze, and the flat loads that
 // result also count in lgkmcnt (every LDS wait of the chains then waits for
@@ -78,9 +78,6 @@ __device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &
     constexpr int N = 4 * Q;  // dwords per chain
     constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};
     uint32_t x[4];
-#if MCRC_NIB == 2
-    const uint32_t par = (c.lane4 & 4u) ? 0x40404040u : 0u;  // odd lane
-#endif
 #pragma unroll
     for (int r = 0; r < 4; ++r) x[r] = it.d[r][0].x;
 #pragma unroll
@@ -90,11 +87,7 @@ __device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &
             if (i + 1 < N) {
                 x[r] = step4_next(x[r], dw4(it.d[r][(i + 1) >> 2], (i + 1) & 3), c);
             } else {
-#if MCRC_NIB == 2
-                x[r] = step4_last_nib2(x[r], r, par);
-#else
                 x[r] = r < 3 ? step4_last_shifted(x[r], kShift[r]) : step4_next(x[r], 0u, c);
-#endif
             }
         }
     }
@@ -136,15 +129,12 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // divergent exit merged an un-waited path there and forced vmcnt(0),
     // which drained the prefetched step).
     uint64_t grp = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
-#if MCRC_K1_CHUNK && MCRC_K1_PERM
     // the ranges dealt to the waves in a scrambled order: wave w takes range
     // (w * 65521) mod W (65521 is prime: a bijection unless it divides W), so
     // a CU's 16 waves stream ranges far apart rather than 16 neighbouring
     // MiB: -0.6 % at 1 and 4 Mi items in every round
     // (profiles/r04_ablations/k1_range_order_ab.txt)
     if (gstep % 65521u) grp = (grp * 65521u) % gstep;
-#endif
-#if MCRC_K1_CHUNK
     // wave w takes the contiguous groups [w cg, (w + 1) cg): 1.0-1.4 % faster
     // than the grid-stride order at 1 Mi items, 0.6-3.7 % at 4 Mi, on two
     // boxes (profiles/r04_ablations/k1_chunk_and_census_ab.txt,
@@ -155,10 +145,6 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     grp *= cg;
     if (grp >= ngroups) return;
     const uint64_t gs = 1, glast = gend - 1;
-#else
-    if (grp >= ngroups) return;
-    const uint64_t gs = gstep;
-#endif
     auto item_of = [&](uint64_t gi) { return gi * IPW + g; };
 
     Regs ra, rb;
@@ -170,11 +156,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // the step: left alone, the scheduler sinks them into the chains and the
     // next step waits on loads issued moments before.
     auto ld = [&](Regs &r, uint64_t gi) {
-#if MCRC_K1_CHUNK
         const uint64_t gu = gi < gend ? gi : glast;
-#else
-        const uint64_t gu = gi < ngroups ? gi : gi - gstep < ngroups ? gi - gstep : ngroups - 1;
-#endif
         const uint64_t first = gu * IPW;
         const uint8_t *wb = base + first * stride;
         const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
@@ -193,11 +175,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // One exit, at the bottom of each loop: a break between the halves would
     // give the loop header a second (un-waited) predecessor, and the waitcnt
     // pass would then drain every prefetched load there.
-#if MCRC_K1_CHUNK
     const uint64_t nsteps = (gend - grp + gs - 1) / gs;
-#else
-    const uint64_t nsteps = (ngroups - grp + gstep - 1) / gstep;
-#endif
     ld(ra, grp);
     uint64_t k = 0;
     for (; k + 4 <= nsteps; k += 4) {
@@ -791,9 +769,6 @@ template <int NS>
 __device__ __forceinline__ uint32_t block_value(const BlockWin &w, const LaneCtx &c) {
     constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};
     uint32_t x[4];
-#if MCRC_NIB == 2
-    const uint32_t par = (c.lane4 & 4u) ? 0x40404040u : 0u;  // odd lane
-#endif
 #pragma unroll
     for (int r = NS; r < 4; ++r) x[r] = w.v[r][0].x;
 #pragma unroll
@@ -803,11 +778,7 @@ __device__ __forceinline__ uint32_t block_value(const BlockWin &w, const LaneCtx
             if (i + 1 < 8) {
                 x[r] = step4_next(x[r], dw4(w.v[r][(i + 1) >> 2], (i + 1) & 3), c);
             } else {
-#if MCRC_NIB == 2
-                x[r] = step4_last_nib2(x[r], r, par);
-#else
                 x[r] = r < 3 ? step4_last_shifted(x[r], kShift[r]) : step4_next(x[r], 0u, c);
-#endif
             }
         }
     }
@@ -1743,34 +1714,12 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
 }
 
 // ===========================================================================
-// K5: one-block item images end to end (k_items)
+// K5: shared pieces (item images or equal spans whose span is one 4 KiB
+// window after a short head; the kernel is k_lines below)
 // ===========================================================================
 //
-// The planned path spends a pass per image before k_blocks (k_count: the
-// header, the head fragment and the tail piece) plus a select, an expansion
-// and k_final.  For images whose span is one 4 KiB block after a head
-// fragment of 4..kFragMax bytes (every 4165-B image of config 5) k_items
-// does it in one pass, in k_blocks' loop, with the per-image work done once
-// per image by one lane instead of once per step by 32 lanes:
-//   - epochs of 32 steps: at the start of an epoch each lane L of the wave
-//     takes the image of step L / 2, group L % 2 (the 64 images the wave
-//     checksums in that epoch): its offset, its header (ITEM_ntotal and the
-//     stored CRC, storage.c:567), its block start G = E + t - 4096, and the
-//     register r from ~0 over the head fragment [p, G) -- a per-lane
-//     slice-by-4 chain on this lane's copy of the replicated tables over at
-//     most nine 16-B pieces (bytes below p cleared, ~0 XORed in at p) --
-//     folded to C = M_4096(r) (^ M_t(~stored) for a verify);
-//   - each step, the two groups take G and t of their image from the epoch
-//     lanes (ds_bpermute), load the block, clear the t foreign bytes after E
-//     in lane 31's last piece, and run K1's chains;
-//   - four steps share one lane tree; lanes 0-3 of a group then hold
-//     R = M_t(raw of the span's block) of four images, XOR in their C
-//     (ds_bpermute) and give R ^ C = M_t(f), f the register after the whole
-//     span from ~0: a verify is good iff it is 0 (f == ~stored), a stamp
-//     writes {M_t(f), t} for k_fix, and a MODE 0 span's value goes back to
-//     its epoch lane, which stores ~M_{-t}(M_t(f)) at the end of the epoch.
-// Images that are sane but not of that shape go to a fallback list that the
-// planned path takes afterwards; malformed images are marked bad here.
+// Images that are sane but not of K5's shape go to a fallback list that the
+// planned path takes afterwards; malformed images are marked bad by K5.
 
 struct ItemsOut {
     uint32_t *fb;   // items for the planned path (sane, not one block)
@@ -1781,12 +1730,6 @@ struct ItemsOut {
     uint32_t nsr;        // k_lines: steps per run (a wave's run is 2 nsr consecutive images)
 };
 constexpr uint32_t kRtFused = 0x80000000u;
-
-// The fused shape: one block [Ea - 4096, Ea) after a head fragment of
-// 4..kFragMax bytes (vlen = len + t).
-__host__ __device__ __forceinline__ bool fused_vlen(uint32_t vlen) {
-    return vlen >= kBlockBytes + 4 && vlen - kBlockBytes <= kFragMax;
-}
 
 // The dword at A of the head fragment: bytes below p cleared (pa = p - A)
 // and the four bytes of inj (~c for an initial CRC c: a register seeded with
@@ -1814,253 +1757,19 @@ __device__ __forceinline__ uint32_t zeros_lds(uint32_t v, uint32_t t, const Lane
 
 constexpr uint32_t kStFused = 0x10u, kStSane = 0x20u, kStValid = 0x40u;
 constexpr uint32_t kEpoch = 32;                                 // steps per epoch: 64 images per wave
-constexpr uint32_t kFragPieces = (kFragMax + 15) / 16 + 1;      // 16-B pieces of [floor16(p), G)
 
 struct ItemBuf {
     ItemRegs<32, 32, 4> d;  // the block, rows 0..3
     uint32_t st;            // its image: t | kStFused | kStSane | kStValid
 };
 
-template <int MODE, bool OFFS>
-__global__ __launch_bounds__(1024) void k_items(SpanArgs a, const uint4 *__restrict__ img, ItemsOut io) {
-    // MODE 0: equal spans of a.len bytes by offsets (OFFS) or stride (every
-    // one of the fused shape: the shim checks a.len at every alignment),
-    // MODE 1/2: item images (verify / stamp) by offsets
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint64_t n = a.n;
-    const uint64_t waves = blockDim.x >> 6;
-    const uint64_t gstep = gridDim.x * waves;
-    const uint64_t ngroups = (n + 1) / 2;
-    const uint64_t grp0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
-    if ((uint64_t)blockIdx.x * waves >= ngroups) return;
-    if (MODE != 0 && io.route && *io.route == 0) {  // the census sent the batch to the planned path
-        if (blockIdx.x == 0 && threadIdx.x == 0) *io.nfb = (uint32_t)n;
-        return;
-    }
-    load_tables(smem, img, kLdsImageK1Bytes);
-    if (grp0 >= ngroups) return;
-    const uint32_t lane = threadIdx.x & 63u, li = lane & 31u, g = lane >> 5;
-    LaneCtx c;
-    c.lane4 = li << 2;
-    c.lane4hi = c.lane4 | 0x10000u;
-    gbyte *const gb = (gbyte *)a.base;
-    gbyte *const gz = (gbyte *)(a.zero + (blockIdx.x % kZeroSlots) * (4096 / 16));
-    const uint32_t base_lo = (uint32_t)(uintptr_t)a.base;  // (for alignments: the offsets are from a.base)
-    const uint64_t nsteps = (ngroups - grp0 + gstep - 1) / gstep;
-    uint32_t nb = 0;  // bad (malformed or mismatching) images seen by this lane
-    // this lane's image of the epoch: block offset from a.base (lo, hi), status, C
-    uint32_t eglo = 0, eghi = 0, est = 0, ec = 0;
-
-    // The epoch starting at step e0 of this wave: lane L prepares the image
-    // of step e0 + L / 2, group L % 2, in three stages so that the first
-    // block's loads overlap the fragment chain: prep_head (offset -- loaded
-    // during the previous epoch -- header, shape, block address), the
-    // fragment's piece loads, then (after the epoch's first block load is
-    // issued) prep_chain.
-    auto item_of = [&](uint64_t e0) -> uint64_t { return (grp0 + (e0 + (lane >> 1)) * gstep) * 2 + (lane & 1u); };
-    auto valid_of = [&](uint64_t e0) { return e0 + (lane >> 1) < nsteps && item_of(e0) < n; };
-    auto off_of = [&](uint64_t e0) -> uint64_t {
-        // (offsets or stride is a template choice: a load on one side of a
-        // branch leaves the waitcnt pass a merged state that waits for it)
-        return valid_of(e0) ? (OFFS ? a.offsets[item_of(e0)] : item_of(e0) * a.stride) : 0;
-    };
-    // MODE 0: x^(-8t), t < 16, lane-distributed (lane j holds t = j & 15);
-    // loaded before the first epoch's loads, so their waits retire it
-    const uint32_t xinv = MODE == 0 ? a.xpow[kXpowInv + (lane & 15u)] : 0u;
-    uint64_t noff = off_of(0);  // the offset of this lane's image in the next epoch
-    uint32_t ncin = MODE == 0 && a.crc_in && valid_of(0) ? a.crc_in[item_of(0)] : 0u;
-    // stage state
-    uint32_t p_kh = 0, p_t = 0, p_np16 = 0, p_inj = ~0u, p_stored = 0;
-    uint64_t p_pho = 0;
-    uint4 pc[kFragPieces];
-    auto prep_head = [&](uint64_t e0) {
-        const bool valid = valid_of(e0);
-        const uint64_t off = noff;
-        ItemHdr h{0u, 0u, 0u, 0u};
-        ItemDesc it{a.base, 0u, 0u, false};
-        p_inj = ~0u;  // ~c: the register's initial value, XORed in at p
-        if (MODE == 0) {
-            it.sane = valid && off <= a.base_bytes && a.len <= a.base_bytes - off;
-            it.len = a.len;
-            if (a.crc_in) p_inj = ~ncin;
-        } else {
-            const bool hdr_ok = valid && off + 48 <= a.base_bytes;
-            if (hdr_ok) h = parse_hdr(gb + off);
-            it = item_desc(a, off, h, hdr_ok);
-        }
-        p_stored = h.exptime;
-        const uint32_t len = it.sane ? it.len : 0u;
-        const uint64_t po = MODE == 0 ? off : off + 32;             // span start (offset)
-        p_kh = (base_lo + (uint32_t)po) & 15u;                     // its alignment
-        p_t = (0u - p_kh - len) & (kTailAlign - 1);                 // tail_pad
-        const uint32_t vlen = len + p_t;
-        const bool fused = it.sane && fused_vlen(vlen);
-        const uint64_t go = po + vlen - kBlockBytes;                // block start (offset)
-        p_pho = po - p_kh;
-        p_np16 = fused ? (uint32_t)(go - p_pho) >> 4 : 0u;
-        eglo = (uint32_t)go;
-        eghi = (uint32_t)(go >> 32);
-        est = p_t | (fused ? kStFused : 0u) | (it.sane ? kStSane : 0u) | (valid ? kStValid : 0u);
-    };
-    // the fragment's pieces (a lane whose span is not fused reads zeros)
-    auto prep_pieces = [&]() {
-#pragma unroll
-        for (uint32_t k = 0; k < kFragPieces; ++k) pc[k] = ld16(k < p_np16 ? gb + p_pho + 16 * k : gz);
-    };
-    // r = register from ~c over [p, G): the pieces of [floor16(p), G), bytes
-    // below p cleared and ~c injected at p (head_dword); C = M_4096(r)
-    auto prep_chain = [&]() {
-        uint32_t x = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kFragPieces; ++k) {
-            const uint32_t w[4] = {pc[k].x, pc[k].y, pc[k].z, pc[k].w};
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const int32_t pa = (int32_t)p_kh - (int32_t)(16 * k + 4 * j);
-                const uint32_t d = head_dword(w[j], pa, p_inj);
-                const uint32_t nx = (k == 0 && j == 0) ? d : step4_next(x, d, c);
-                x = k < p_np16 ? nx : x;
-            }
-        }
-        x = p_np16 ? step4_next(x, 0u, c) : 0u;  // (past the last dword)
-        uint32_t cc = apply_op<4>(kAuxSpanFold, x);  // M_4096(r): the block follows
-        if (MODE == 1) cc ^= zeros_lds(~p_stored, p_t, c);  // (R ^ C == 0 iff the stored CRC matches)
-        ec = p_np16 ? cc : 0u;
-    };
-    // Loads of step s (< ns, else a repeat of the epoch's last step, whose
-    // result is not used) into b: its block and its status.
-    auto ld = [&](ItemBuf &b, uint32_t s, uint32_t ns) {
-        const int src = (int)(2 * min(s, ns - 1) + g);
-        const uint64_t lo = (uint32_t)__shfl((int)eglo, src, 64), hi = (uint32_t)__shfl((int)eghi, src, 64);
-        b.st = (uint32_t)__shfl((int)est, src, 64);
-        gbyte *blk = (b.st & kStFused) ? gb + (lo | (hi << 32)) : gz;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int q = 0; q < 2; ++q) b.d.d[r][q] = ld16(blk + r * 1024 + li * 32 + 16 * q);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto part0 = [&](ItemBuf &b) {
-        if (li == 31u) b.d.d[3][1] = clear_high(b.d.d[3][1], b.st & 15u);
-        return reduce_level<0>(lane_partial_x3s<32>(b.d, c), (lane & 1u) == 0u);
-    };
-    // Result R of step s of the epoch (lanes 0..3 of a group, s < ns): the
-    // image's verdict / stamp record.
-    auto finish = [&](uint32_t raw, uint64_t e0, uint32_t s, uint32_t ns, bool on) -> uint32_t {
-        const int src = (int)(2 * min(s, ns - 1) + g);
-        const uint32_t cq = (uint32_t)__shfl((int)ec, src, 64), st = (uint32_t)__shfl((int)est, src, 64);
-        const uint64_t item = (grp0 + (e0 + s) * gstep) * 2 + g;
-        on = on && s < ns && (st & kStValid);
-        const bool fused = st & kStFused, sane = st & kStSane;
-        const bool fb = MODE != 0 && on && sane && !fused;
-        const uint32_t r = raw ^ cq;  // M_t(f) (verify: 0 iff good)
-        if (on) {
-            if (MODE == 0) {
-                nb += !sane;  // (out of the buffer: not read, out 0, counted; the CRC: emit_epoch)
-            } else if (MODE == 1) {
-                if (fused || !sane) {
-                    const bool good = fused && r == 0u;
-                    a.ok[item] = good;
-                    nb += !good;
-                }
-            } else {
-                io.rt[item] = fused ? make_uint2(r, (st & 15u) | kRtFused) : make_uint2(0u, 0u);
-                if (!sane) {
-                    if (a.ok) a.ok[item] = 0;
-                    ++nb;
-                }
-            }
-        }
-        if (MODE != 0) {
-            const uint64_t m = __ballot(fb);  // the fallback list: one atomic per wave with entries
-            if (m) {
-                const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-                uint32_t base = 0;
-                if (lane == first) base = atomicAdd(io.nfb, (uint32_t)__popcll(m));
-                base = __shfl(base, (int)first, 64);
-                if (fb) io.fb[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)item;
-            }
-        }
-        return r;
-    };
-    // MODE 0: the epoch lanes collect R ^ C = M_t(f) of their images from the
-    // lanes that finished them (steps s0 .. s0 + cnt - 1 in lanes 0 .. cnt - 1
-    // of each group), and at the end of the epoch each lane stores the CRC of
-    // its image, ~M_{-t}(M_t(f)) -- one multiply per image by one lane, in
-    // place of a pass over the batch (k_fix).
-    uint32_t er = 0;
-    auto collect = [&](uint32_t r, uint32_t s0, uint32_t cnt) {
-        const uint32_t sl = lane >> 1;
-        const int src = (int)((lane & 1u) * 32u + (sl - s0));
-        const uint32_t v = (uint32_t)__shfl((int)r, sl - s0 < cnt ? src : 0, 64);
-        er = sl - s0 < cnt ? v : er;
-    };
-    auto emit_epoch = [&](uint64_t e0) {
-        const uint32_t xt = (uint32_t)__shfl((int)xinv, (int)(est & 15u), 64);
-        if (valid_of(e0)) a.out[item_of(e0)] = (est & kStFused) ? ~mulmodp_dev(er, xt) : 0u;
-    };
-    ItemBuf ra, rb;
-    for (uint64_t e0 = 0; e0 < nsteps; e0 += kEpoch) {
-        const uint32_t ns = (uint32_t)min((uint64_t)kEpoch, nsteps - e0);
-        prep_head(e0);
-        prep_pieces();
-        // the next epoch's offsets (and initial CRCs), consumed one epoch later
-        noff = off_of(e0 + kEpoch);
-        if (MODE == 0) ncin = a.crc_in && valid_of(e0 + kEpoch) ? a.crc_in[item_of(e0 + kEpoch)] : 0u;
-        ld(ra, 0, ns);
-        prep_chain();
-        uint32_t s = 0;
-        for (; s + 4 <= ns; s += 4) {
-            ld(rb, s + 1, ns);
-            const uint32_t va = part0(ra);
-            ld(ra, s + 2, ns);
-            const uint32_t vb = part0(rb);
-            const uint32_t vab = group_pair_level1(va, vb, lane);
-            ld(rb, s + 3, ns);
-            const uint32_t vc = part0(ra);
-            ld(ra, s + 4, ns);
-            const uint32_t vd = part0(rb);
-            const uint32_t raw = group_reduce32_quad_span(vab, group_pair_level1(vc, vd, lane), lane);
-            const uint32_t r = finish(raw, e0, s + (li & 3u), ns, li < 4);
-            if (MODE == 0) collect(r, s, 4);
-        }
-        for (; s + 2 <= ns; s += 2) {
-            ld(rb, s + 1, ns);
-            const uint32_t va = part0(ra);
-            ld(ra, s + 2, ns);
-            const uint32_t vb = part0(rb);
-            const uint32_t raw = group_reduce32_pair_span(va, vb, lane);
-            const uint32_t r = finish(raw, e0, s + (li & 1u), ns, li < 2);
-            if (MODE == 0) collect(r, s, 2);
-        }
-        if (s < ns) {
-            const uint32_t v = part0(ra);
-            // (part0 ran level 0; levels 1..4 of the span tree)
-            uint32_t r = reduce_level<1>(v, (lane & 3u) == 0u);
-            r = reduce_level<2>(r, (lane & 7u) == 0u);
-            r = reduce_level<3>(r, (lane & 15u) == 0u);
-            r = reduce_level4_span(r, (lane & 31u) == 0u);
-            r = finish(r, e0, s, ns, li == 0);
-            if (MODE == 0) collect(r, s, 1);
-        }
-        if (MODE == 0) emit_epoch(e0);
-    }
-    // one atomic per wave for the bad count
-    nb += __shfl_xor(nb, 1);
-    nb += __shfl_xor(nb, 2);
-    nb += __shfl_xor(nb, 4);
-    nb += __shfl_xor(nb, 8);
-    nb += __shfl_xor(nb, 16);
-    nb += __shfl_xor(nb, 32);
-    if (lane == 0 && nb) atomicAdd(a.nbad, (unsigned long long)nb);
-}
-
 // ===========================================================================
 // K5, line-anchored (k_lines, round 4)
 // ===========================================================================
 //
-// k_items reads each image's header and head fragment at the start of an
-// epoch and the image's 16-B-anchored block up to 32 steps later, by when the
+// Round 3's K5 (k_items, removed in round 5; git show 7745007) read each
+// image's header and head fragment at the start of an epoch and the image's
+// 16-B-anchored block up to 32 steps later, by when the
 // lines they share (the block's first line, the previous block's last line,
 // which holds this image's header) have left L2: config 5 fetched 1.08x its
 // span bytes, config 2r 1.065x (profiles/r04_ablations).  Here no line is
@@ -2118,18 +1827,11 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
     // slower: profiles/r04_ablations/k5_lines_stagger_ab.txt.)
     // tests/test_items_lines_model.py checks that the runs cover every image
     // exactly once.
-#if MCRC_K5_CHUNK
     const uint64_t C = ((n + W - 1) / W + 1) & ~1ull;
     const uint64_t f0 = 1 + w0 % nsr, cend = min((w0 + 1) * C, n);
     auto run_start = [&](uint64_t k) -> uint64_t { return w0 * C + (k == 0 ? 0 : 2 * (f0 + (k - 1) * nsr)); };
     auto run_steps = [&](uint64_t k) -> uint64_t { return k == 0 ? f0 : nsr; };
     if ((uint64_t)blockIdx.x * waves * C >= n) return;
-#else
-    auto run_start = [&](uint64_t k) -> uint64_t { return (k * W + w0) * run_imgs; };
-    auto run_steps = [&](uint64_t) -> uint64_t { return nsr; };
-    const uint64_t cend = n;
-    if ((uint64_t)blockIdx.x * waves * run_imgs >= n) return;
-#endif
     if (MODE != 0 && io.route && *io.route == 0) {  // the census sent the batch to the planned path
         if (blockIdx.x == 0 && threadIdx.x == 0) *io.nfb = (uint32_t)n;
         return;
@@ -2371,28 +2073,24 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
 // The last step of a K5 stamp (MODE 2), one thread per image: from R = M_t(f),
 // f the register after the span from ~0, the CRC is ~M_{-t}(R), stamped into
 // the image's exptime as the spill CRC (storage.c:567).  A separate pass:
-// within k_items an image's stamp could race with another wave's read of the
+// within k_lines an image's stamp could race with another wave's read of the
 // same bytes when images overlap.  (MODE 0 spans get their CRC from the epoch
-// lanes of k_items itself.)
+// lanes of k_lines itself.)
 __global__ void k_fix(SpanArgs a, const uint2 *rt, const uint32_t *route) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
-    if (route && *route == 0) return;  // (k_items took no image)
+    if (route && *route == 0) return;  // (k_lines took no image)
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint2 r = rt[i];
         if (r.y & kRtFused) {
             const uint32_t crc = ~mulmodp_dev(r.x, a.xpow[kXpowInv + (r.y & 15u)]);
             uint8_t *p = const_cast<uint8_t *>(a.base) + a.offsets[i] + 32;
-#if MCRC_FIX_NT
             // non-temporal: plain stores left 16 M dirty 32-B sectors in the
             // caches, written back while the next batch streamed (its
             // k_lines<2> 0.11 ms slower per 300 pages); so the write-backs
             // happen here (k_fix 0.17 -> 0.25 ms), stamp -1.2 % in all
             // (profiles/r04_ablations/k_fix_nontemporal_ab.txt)
             for (int b = 0; b < 4; ++b) __builtin_nontemporal_store((uint8_t)(crc >> (8 * b)), p - 4 + b);
-#else
-            __builtin_memcpy(p - 4, &crc, 4);
-#endif
             if (a.ok) a.ok[i] = 1;
         }
     }
@@ -2404,7 +2102,7 @@ __global__ void k_fix(SpanArgs a, const uint2 *rt, const uint32_t *route) {
 // the batch, and *route = 1 when at least 15/16 of them have K5's shape (one
 // 4 KiB block after a short head fragment).  Below that the images K5 leaves
 // to its fallback cost a second pass, and the planned path takes the batch
-// (k_items then lists every image).  One workgroup, one header per thread.
+// (k_lines then lists every image).  One workgroup, one header per thread.
 constexpr uint32_t kCensus = 1024;
 template <int MODE>
 __global__ __launch_bounds__(kCensus) void k_census(SpanArgs a, uint32_t *route) {
@@ -2416,13 +2114,9 @@ __global__ __launch_bounds__(kCensus) void k_census(SpanArgs a, uint32_t *route)
     if (threadIdx.x < s) {
         const uint64_t i = threadIdx.x * n / s;
         const ItemDesc it = fetch_item<MODE>(a, i);
-#if MCRC_K5_ITEMS
-        const bool fused = fused_vlen(it.len + tail_pad(it.p, it.len));
-#else
         const uint64_t pa = (uintptr_t)it.p, A = (pa + 4 + kLineBytes - 1) & ~(uint64_t)(kLineBytes - 1);
         const uint64_t B = (pa + it.len) & ~(uint64_t)(kLineBytes - 1);
         const bool fused = it.len >= 4 && lines_fused((int64_t)B - (int64_t)A);
-#endif
         if (it.sane && fused) atomicAdd(&cnt, 1u);
     }
     __syncthreads();
@@ -2430,7 +2124,7 @@ __global__ __launch_bounds__(kCensus) void k_census(SpanArgs a, uint32_t *route)
 }
 
 // Fallback lists: gather the listed items' offsets / scatter their results.
-// (route 0, k_census: k_items took no image, the list is every image: the
+// (route 0, k_census: k_lines took no image, the list is every image: the
 // identity)
 __global__ void k_gather_offs(const uint64_t *offsets, const uint32_t *idx, const uint32_t *nidx, uint64_t *out,
                               const uint32_t *route) {

@@ -89,7 +89,7 @@ struct Device {
     // images): zero between calls, kept so by the kernel's last workgroup
     unsigned long long *small_nbad = nullptr;
     uint32_t *small_done = nullptr;
-    uint32_t *nfb = nullptr;    // k_items' fallback count (device)
+    uint32_t *nfb = nullptr;    // k_lines' fallback count (device)
     uint32_t *route = nullptr;  // k_census's verdict: K5 (1) or the planned path (0)
     hipStream_t stream = nullptr, copy = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -142,7 +142,11 @@ struct Device {
             if (s.p) (void)hipFree(s.p);
             s.p = nullptr;
             s.bytes = 0;
-            if (hipMalloc(&s.p, bytes) != hipSuccess) return nullptr;
+            if (hipMalloc(&s.p, bytes) != hipSuccess) {
+                s.p = nullptr;
+                (void)hipGetLastError();  // (not left pending for a later launch check)
+                return nullptr;
+            }
             s.bytes = bytes;
         }
         return s.p;
@@ -173,9 +177,16 @@ struct Device {
 };
 enum { kPinStage, kPinOffs, kPinOk, kPinCrc };
 
-std::mutex g_dev_mu;
+std::mutex g_dev_mu;  // device discovery and first initialisation only
 std::vector<std::unique_ptr<Device>> g_devs;
 int g_ndev = -1;
+// Initialised devices by id, published once (release) after init_device: the
+// per-call lookup reads them without g_dev_mu, so threads driving different
+// devices (crc32c_batch_multi, IO threads on several GPUs) never serialise on
+// a process-wide lock after the first call.
+constexpr int kMaxDevices = 64;
+std::atomic<Device *> g_ready[kMaxDevices];
+std::atomic<int> g_ndev_pub{-1};
 
 // MCRC_DEBUG=1 in the environment: report the failing HIP call on stderr.
 bool debug_on() {
@@ -291,10 +302,6 @@ int init_device(Device &d, int id) {
         (const void *)mcrc_dev::k_blocks<false, true>,
         (const void *)mcrc_dev::k_blocks<true, true>,
         (const void *)mcrc_dev::k_blocks<true, false>,
-        (const void *)mcrc_dev::k_items<0, true>,
-        (const void *)mcrc_dev::k_items<0, false>,
-        (const void *)mcrc_dev::k_items<1, true>,
-        (const void *)mcrc_dev::k_items<2, true>,
         (const void *)mcrc_dev::k_lines<0, true>,
         (const void *)mcrc_dev::k_lines<0, false>,
         (const void *)mcrc_dev::k_lines<1, true>,
@@ -308,16 +315,24 @@ int init_device(Device &d, int id) {
 
 int ensure_devices() {  // (call with g_dev_mu held)
     if (g_ndev < 0) {
-        g_ndev = count_gfx950();
+        g_ndev = std::min(count_gfx950(), kMaxDevices);
         for (int i = 0; i < g_ndev; ++i) g_devs.emplace_back(new Device());
+        g_ndev_pub.store(g_ndev, std::memory_order_release);
     }
     return g_ndev;
 }
 
-// Device state for the calling thread's current HIP device.
+// Device state for the calling thread's current HIP device.  After a
+// device's first call this is hipGetDevice plus one acquire load.
 int current_device(Device **out) {
     int id = 0;
     if (hipGetDevice(&id) != hipSuccess) return CRC32C_ENODEV;
+    if (id >= 0 && id < kMaxDevices) {
+        if (Device *r = g_ready[id].load(std::memory_order_acquire)) {
+            *out = r;
+            return CRC32C_OK;
+        }
+    }
     std::lock_guard<std::mutex> lk(g_dev_mu);
     ensure_devices();
     if (id < 0 || id >= g_ndev) return CRC32C_ENODEV;
@@ -325,6 +340,7 @@ int current_device(Device **out) {
     if (!d.ok) {
         const int rc = init_device(d, id);
         if (rc != CRC32C_OK) return rc;
+        g_ready[id].store(&d, std::memory_order_release);
     }
     *out = &d;
     return CRC32C_OK;
@@ -338,13 +354,9 @@ int grid_for(const Device &d, uint64_t n) {
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
 // Planned batches split their blocks evenly over the span kernel's 32-lane
-// groups (k_expand's balanced plan).  Built with -DMCRC_SPAN_RR: round robin
-// over units (the A/B baseline).
-#ifdef MCRC_SPAN_RR
-constexpr bool kSpanBalance = false;
-#else
+// groups (k_expand's balanced plan; round robin over units was the round-3
+// A/B baseline, profiles/r03_ablations/k2_balanced_plan_ab.jsonl).
 constexpr bool kSpanBalance = true;
-#endif
 uint32_t span_groups(const Device &d) { return (uint32_t)d.cus * (mcrc_dev::kSpanBlock / 32); }
 
 int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
@@ -396,23 +408,14 @@ bool one_block_len(uint32_t len) {
 }
 
 // Every span of `len` bytes, at any alignment, has K5's fused shape: K5 takes
-// the batch whole (config 2r: 4133-B spans).  k_items: one block after a head
-// fragment of 4..kFragMax bytes (mcrc_dev::fused_vlen), at every 16-B
-// alignment; k_lines: 31 or 32 whole lines after a 4..131-B head, at every
-// 128-B alignment.
+// the batch whole (config 2r: 4133-B spans).  k_lines: 31 or 32 whole lines
+// after a 4..131-B head, at every 128-B alignment.
 bool fused_len(uint32_t len) {
-#if MCRC_K5_ITEMS
-    for (uint32_t kh = 0; kh < 16; ++kh) {
-        const uint32_t vlen = len + ((0u - kh - len) & (mcrc_dev::kTailAlign - 1));
-        if (!mcrc_dev::fused_vlen(vlen)) return false;
-    }
-#else
     constexpr uint32_t L = mcrc_dev::kLineBytes;
     for (uint32_t al = 0; al < L; ++al) {
         const int64_t A = (al + 4 + L - 1) / L * L, B = (al + (int64_t)len) / L * L;
         if (len < 4 || !mcrc_dev::lines_fused(B - A)) return false;
     }
-#endif
     return true;
 }
 
@@ -421,16 +424,11 @@ bool fused_len(uint32_t len) {
 template <int MODE, bool OFFS>
 void launch_k5(const Device &d, const mcrc_dev::SpanArgs &a, mcrc_dev::ItemsOut io, hipStream_t st) {
     const int grid = grid_for(d, a.n);
-#if MCRC_K5_ITEMS
-    hipLaunchKernelGGL((mcrc_dev::k_items<MODE, OFFS>), dim3(grid), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st, a,
-                       d.img, io);
-#else
     const uint64_t waves = (uint64_t)grid * (1024 / 64);
     io.xk = d.xk;
     io.nsr = (uint32_t)std::min<uint64_t>(mcrc_dev::kEpoch, std::max<uint64_t>(1, (a.n + 2 * waves - 1) / (2 * waves)));
     hipLaunchKernelGGL((mcrc_dev::k_lines<MODE, OFFS>), dim3(grid), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st, a,
                        d.img, io);
-#endif
 }
 
 // Large item batches go through launch_items, where k_census samples their
@@ -590,7 +588,7 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
 
 // K5 over the item images of a (MODE 1 verify, MODE 2 stamp; device memory,
 // a.nbad zeroed by the caller): k_census routes the batch on the device,
-// k_items checksums the one-block images (+ k_fix for stamps) and lists the
+// k_lines checksums the one-block images (+ k_fix for stamps) and lists the
 // others, and the planned path takes that list with its length read on the
 // device (a.dn).  Nothing is read back: an async stamp stays async.
 template <int MODE>
@@ -1155,12 +1153,16 @@ struct Queue {
         if (worker.joinable()) worker.join();
     }
 
-    void submit(crc32c_job *j) {
+    // false once the dispatcher is stopping (process exit): a job queued
+    // then might never run, so it is refused instead
+    bool submit(crc32c_job *j) {
         {
             std::lock_guard<std::mutex> lk(mu);
+            if (stop) return false;
             pending.push_back(j);
         }
         cv_work.notify_one();
+        return true;
     }
 
     // Completion wakes exactly the job's own waiter (a futex on j->done): with
@@ -1287,6 +1289,7 @@ struct Queue {
 
 // Every device's dispatcher stops (after its pending jobs) at process exit.
 void stop_queues() {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
     for (auto &d : g_devs)
         if (Queue *q = d->queue.load(std::memory_order_acquire)) q->shutdown();
 }
@@ -1349,6 +1352,8 @@ int make_job(const crc32c_spans &s, unsigned flags, crc32c_job **out) {
 extern "C" {
 
 int crc32c_gpu_count(void) {
+    const int n = g_ndev_pub.load(std::memory_order_acquire);
+    if (n >= 0) return n;
     std::lock_guard<std::mutex> lk(g_dev_mu);
     return ensure_devices();
 }
@@ -1403,7 +1408,11 @@ int crc32c_batch_submit(const crc32c_spans *s, unsigned flags, crc32c_job_t *job
     crc32c_job *j = nullptr;
     const int rc = make_job(*s, flags, &j);
     if (rc) return rc;
-    j->q->submit(j);
+    if (!j->q->submit(j)) {
+        if (j->after) (void)hipEventDestroy(j->after);
+        delete j;
+        return CRC32C_EHIP;
+    }
     *job = j;
     return CRC32C_OK;
 }
@@ -1441,8 +1450,7 @@ int crc32c_batch(const crc32c_spans *s, unsigned flags, void *stream) {
             delete j;
             return run_host_batch(*d, *s);
         }
-        j->q->submit(j);
-        rc = j->q->wait(j);
+        rc = j->q->submit(j) ? j->q->wait(j) : CRC32C_EHIP;
         delete j;
         return rc;
     }
@@ -1570,10 +1578,13 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     mcrc_dev::WalkOut wo{};
     wo.cnt = cnt;
     // the count pass keeps each wbuf's first offsets (one per 2 KiB of wbuf:
-    // every 4 MiB wbuf of items of at least 2 KiB), so a K5 verify's emit pass
-    // copies them instead of walking again
-    wo.kslot = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(wbuf_bytes / 2048, 64), 8192);
-    wo.slots = (uint64_t *)d->grow(kScrWalkSlots, (size_t)nw * wo.kslot * 8);
+    // every 4 MiB wbuf of items of at least 2 KiB; 8 B per 2 KiB, 0.4 % of the
+    // walked bytes), so a K5 verify's emit pass copies them instead of walking
+    // again.  Wbufs under 16 KiB keep none (walked twice), and so does a walk
+    // whose slot buffer cannot be allocated.
+    wo.kslot = (uint32_t)std::min<uint64_t>(wbuf_bytes / 2048, 8192);
+    if (wo.kslot < 8) wo.kslot = 0;
+    wo.slots = wo.kslot ? (uint64_t *)d->grow(kScrWalkSlots, (size_t)nw * wo.kslot * 8) : nullptr;
     if (!wo.slots) wo.kslot = 0;
     HIP_OK(hipMemsetAsync(cnt + nw, 0, 4, st));
     hipLaunchKernelGGL(mcrc_dev::k_walk<false>, dim3(gw), bw, 0, st, a, nw, wo);

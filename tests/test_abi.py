@@ -128,3 +128,20 @@ def test_python_constants_match_the_header():
     assert not hasattr(_lib, "CRC32C_ALIGNED16")  # retired: no kernel read it
     for name, val in defs.items():
         assert getattr(_lib, name) == int(val, 0), name
+
+
+def test_batch_accepts_the_retired_aligned16_keyword():
+    """batch(aligned16=...) still parses (a DeprecationWarning, no effect):
+    with a GPU the CRCs are the oracle's, without one the call fails with
+    ENODEV, not a TypeError."""
+    from tests import oracle
+    buf = np.random.default_rng(3).integers(0, 256, 1 << 14, dtype=np.uint8)
+    offs = np.array([0, 16, 4096], np.uint64)
+    lens = np.array([100, 4096, 33], np.uint32)
+    with pytest.warns(DeprecationWarning):
+        try:
+            got = mc.batch(buf, offsets=offs, lens=lens, aligned16=True)
+        except _lib.Crc32cError as e:
+            assert e.rc == _lib.CRC32C_ENODEV and _lib.lib.crc32c_gpu_count() == 0
+            return
+    np.testing.assert_array_equal(got, oracle.batch(buf, offs, lens))

@@ -276,6 +276,57 @@ def test_batch_multi_config4_shape_every_device(torch):
             np.testing.assert_array_equal(out, want)
 
 
+def test_eight_threads_concurrent_device_batches(torch):
+    """Eight host threads each enqueue device batches on their own stream at
+    once (thread t on device t % device_count: every device where the box has
+    several), mixing K1 items, unaligned spans and async calls, many rounds:
+    the per-call device lookup takes no process-wide lock after the first call
+    (crc32c_shim.hip current_device) and no batch sees another's scratch.
+    Every CRC against the oracle."""
+    ng = torch.cuda.device_count()
+    rng = np.random.default_rng(88)
+    nthreads, rounds = 8, 12
+    host = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    n1 = 512  # K1: 512 aligned 4 KiB items
+    want1 = oracle.batch(host, np.arange(n1, dtype=np.uint64) * 4096, np.full(n1, 4096, np.uint64))
+    lens = rng.integers(0, 20000, 400).astype(np.uint32)
+    offs = rng.integers(0, host.size - 20000, 400).astype(np.uint64)
+    want2 = oracle.batch(host, offs, lens)
+    errors = []
+
+    def worker(t):
+        try:
+            dev = t % ng
+            with torch.cuda.device(dev):
+                st = torch.cuda.Stream(device=dev)
+                d = torch.from_numpy(host).to(f"cuda:{dev}")
+                d_offs = torch.from_numpy(offs.view(np.int64)).to(f"cuda:{dev}")
+                d_lens = torch.from_numpy(lens.view(np.int32)).to(f"cuda:{dev}")
+                torch.cuda.synchronize(dev)
+                for r in range(rounds):
+                    with torch.cuda.stream(st):
+                        out1 = torch.empty(n1, dtype=torch.int32, device=f"cuda:{dev}")
+                        sp = _lib.Spans(d.data_ptr(), n1 * 4096, None, 4096, None, 4096, None, out1.data_ptr(), n1)
+                        flags = _lib.CRC32C_DEVICE | (_lib.CRC32C_ASYNC if r % 2 else 0)
+                        _lib.check(_lib.lib.crc32c_batch(ctypes.byref(sp), flags, ctypes.c_void_p(st.cuda_stream)))
+                        out2 = mc.batch(d, offsets=d_offs, lens=d_lens, stream=st.cuda_stream,
+                                        asynchronous=bool(r % 3 == 1))
+                    st.synchronize()
+                    if not (out1.cpu().numpy().view(np.uint32) == want1).all():
+                        errors.append((t, r, "K1"))
+                    if not (out2.cpu().numpy().view(np.uint32) == want2).all():
+                        errors.append((t, r, "spans"))
+        except Exception as e:  # noqa: BLE001  (reported by the main thread)
+            errors.append((t, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:8]
+
+
 def test_bench_headline_over_every_device_in_one_process(torch):
     """bench.py --gpus N without a launcher (the driver's way of starting it):
     headline_devices runs K1 on every visible device from one process and

@@ -578,6 +578,31 @@ def test_verify_pages_tiny_wbufs(torch, wbuf):
         assert nbad == int((got_ok.cpu().numpy() == 0).sum())
 
 
+@pytest.mark.parametrize("wbuf", [8 << 10, 16 << 10])
+def test_verify_pages_k5_small_wbufs_walked_twice(torch, wbuf):
+    """K5-shaped images (4165 B) in wbufs of one to three images, 4200 of
+    them: 8 KiB wbufs keep no walk slots (the emit pass walks every wbuf
+    again), 16 KiB wbufs keep 8 each; both give the sequential walk's items
+    and the oracle's verdicts, with 1 % of the images corrupted."""
+    rng = np.random.default_rng(wbuf)
+    items = [layout.make_item(b"key%07d" % i, rng.integers(0, 256, 4096, dtype=np.uint8).tobytes(), cas=i + 1)
+             for i in range(4200)]
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    ok, nbad = mc.stamp_items(buf, offs, region_bytes=wbuf)
+    assert nbad == 0
+    bad = rng.choice(offs.size, 42, replace=False)
+    for i in bad:
+        buf[int(offs[i]) + 100 + int(rng.integers(0, 3000))] ^= 1 << int(rng.integers(0, 8))
+    want = _walk(buf, wbuf)
+    np.testing.assert_array_equal(want, offs)
+    got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, buf), wbuf)
+    np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), want)
+    expect = np.ones(offs.size, bool)
+    expect[bad] = False
+    np.testing.assert_array_equal(got_ok.cpu().numpy().astype(bool), expect)
+    assert nbad == bad.size
+
+
 def test_chained_iovs(torch):
     """Chunked items (storage.c:163-170): the CRC chained over an item's iovs
     (header from +32, then each chunk) equals crc32c(0, concatenation)."""

@@ -57,7 +57,7 @@ def test_every_kernel_allocates_at_least_32_vgprs(tmp_path):
     assert all("mcrc_dev" in n for n in ks), [n for n in ks if "mcrc_dev" not in n]
     # every kernel of crc32c_kernels.hip is in the library
     for k in ("k_fixed", "k_spans", "k_count", "k_expand", "k_expand_big", "k_final", "k_small", "k_blocks",
-              "k_items", "k_fix", "k_gather_offs", "k_scatter_ok", "k_chain", "k_walk", "k_plan_tiles",
+              "k_fix", "k_gather_offs", "k_scatter_ok", "k_chain", "k_walk", "k_plan_tiles",
               "k_plan_scan", "k_scan32", "k_census", "k_lines"):
         assert any(re.search(rf"\d{k}E", n) or re.search(rf"\d{k}I", n) for n in ks), k
     low = {n: v for n, (v, a, _) in ks.items() if ((v + 7) // 8) * 8 < 32}
@@ -67,3 +67,16 @@ def test_every_kernel_allocates_at_least_32_vgprs(tmp_path):
     for n, (v, a, lds) in ks.items():
         if any(f"{len(k)}{k}" in n for k in ("k_fix", "k_gather_offs", "k_scatter_ok", "k_chain")):
             assert v <= 64, (n, v)
+
+
+def test_no_build_switch_alternatives_in_the_product_sources():
+    """One build of the product: no #if/#ifdef feature switch selects an
+    untested alternative kernel path (round-4 review item 5)."""
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "memcached_amd", "csrc")
+    bad = []
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h", ".cpp")):
+            for i, line in enumerate(open(os.path.join(csrc, f)), 1):
+                if re.match(r"\s*#\s*(if|ifdef|ifndef|elif)\b.*MCRC_", line):
+                    bad.append(f"{f}:{i}: {line.strip()}")
+    assert not bad, bad
