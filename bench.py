@@ -421,16 +421,21 @@ def workload_pagesmix(args, rank, world):
         "items_le_4k_frac": round(float((ntot_np <= 4096).mean()), 3), "injected_bad": int(victims.numel())}
 
 
+K1_LAYOUT = "pieces16-nt"  # K1's load shape since round 5 (crc32c_kernels.hip k_fixed)
+
+
 def traffic_per_launch(items=ITEMS_PER_GPU, item_bytes=ITEM_BYTES):
     """HBM bytes per K1 launch from the committed rocprofv3 --pmc summaries:
     the newest profiles/*traffic*.json record of kernel k_fixed measured on
-    this batch shape (files of other kernels or shapes are skipped)."""
+    this batch shape and K1 layout (files of other kernels, shapes or of the
+    earlier K1 are skipped)."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
         try:
             rec = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if (isinstance(rec, dict) and rec.get("kernel") == "k_fixed" and rec.get("items") == items
+        if (isinstance(rec, dict) and rec.get("kernel") == "k_fixed" and rec.get("k1_layout") == K1_LAYOUT
+                and rec.get("items") == items
                 and rec.get("item_bytes") == item_bytes and rec.get("hbm_bytes_per_launch")):
             return rec["hbm_bytes_per_launch"]
     return None
@@ -517,7 +522,8 @@ def headline_result(args, value, elapsed, kernel_ms, n_gpus, settled, parallelis
         "data": f"synthetic ({args.fill} bytes, seed 42 + rank), device-resident",
         "config": {
             "workload": "BASELINE configs[1]: 1 Mi items x 4096 B per GPU, stride 4096, one 32-lane group per "
-                        "item (K1 k_fixed<slice-by-4, 32 lanes, 32 B/lane/row, 4 rows, row folds in the last-step tables, four items reduced per tree>)",
+                        "item (K1 k_fixed<slice-by-4, 32 lanes, 8 x 16-B pieces per lane at 512-B spacing, "
+                        "non-temporal coalesced loads, half-item folds in the last-step tables, four items reduced per tree>)",
             "items_per_gpu": args.items,
             "item_bytes": ITEM_BYTES,
             "parallelism": parallelism,

@@ -26,8 +26,8 @@ namespace mcrc_dev {
 // K1: fixed-length aligned items
 // ===========================================================================
 
-// 16-B load of item bytes.  (Non-temporal loads measured no better for K1 and
-// 5-11 % worse for the span kernels.)
+// 16-B load of item bytes.  (Non-temporal loads: K1 reads through ld16_nt,
+// see k_fixed; they were 5-11 % worse for the span kernels in round 1.)
 __device__ __forceinline__ uint4 ld16(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
 // Global-memory byte and piece pointers.  k_lines keeps its addresses in
 // these: derived from the kernel arguments through generic pointers, they
@@ -38,6 +38,13 @@ typedef const __attribute__((address_space(1))) uint8_t gbyte;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld16(gbyte *p) {
     const u32x4 v = *(const __attribute__((address_space(1))) u32x4 *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Non-temporal 16-B load (the `nt` policy bit: the line is streamed, not kept
+// in L2 / the Infinity Cache).
+__device__ __forceinline__ uint4 ld16_nt(const uint8_t *p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -96,16 +103,55 @@ __device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &
 
 // K1 geometry: a 32-lane group owns one 4096-B item (4 rows of 1 KiB, lane i
 // owns bytes [32 i, 32 i + 32) of each row), a wave two items per step.
-constexpr uint32_t kK1Rows = 4, kK1CH = 32, kK1Bytes = kK1Rows * 32 * kK1CH;
+constexpr uint32_t kK1Rows = 4, kK1CH = 32, kK1Bytes = kK1Rows * 32 * kK1CH;  // (the row layout: k_lines)
 
-// Persistent grid-stride loop over equal 4 KiB items at a fixed stride:
-//   out[i] = crc32c(crc_in ? crc_in[i] : 0, base + i * stride, 4096).
-// Per item: ~crc_in is XORed into the item's first data dword (a register
-// seeded with ~crc_in adds exactly M_len(~crc_in), crc32c.c:166, so
-// crc32c(crc_in, D) = ~raw(D ^ (~crc_in || 0...)) -- no multiply), the lane
-// partials are the four row chains' XOR, and four consecutive steps of the
-// wave are reduced by one lane tree (group_pair_level1 + group_reduce32_quad).
-// Loads run one step ahead in two register sets (no copies).
+// K1's lane layout (round 5).  A 32-lane group owns one 4096-B item, and lane
+// i holds the 16-B pieces at 512 k + 16 i, k = 0..7: each load instruction
+// reads 512 contiguous bytes per group (two items, 1 KiB per wave), so every
+// 128-B line is read whole by one instruction.  With non-temporal loads that
+// reads 4 GiB at 82-83 % of the HBM peak, against 73-76 % for the 32-B-per-
+// lane rows of rounds 1-4 (lane i at 32 i + 16 q of each KiB, two
+// instructions per line) and 69-71 % for either shape with the default
+// policy (profiles/r05_k1_ceiling.txt).  Algebra: the piece at 512 k + 16 i
+// stands M_{512 (7-k) + 16 (31-i)} from the item's end.  Lane i runs one
+// four-dword chain per piece; the chains of each half item fold through the
+// shifted last steps M_1536, M_1024, M_512 (and the plain step), the first
+// half moves up by M_2048, and the lane tree merges 16-B granules (levels
+// M_16 .. M_128; level 4 = level 3 twice).  Table image: build_lds_image_span
+// at chunk 16 (crc32c_gf2.h): tree at tables 0..15, M_2048 at 16..19, the
+// shifted steps at kAuxShift2 / kAuxShift1 / kAuxShift0.
+constexpr uint32_t kK1Pieces = 8, kK1Piece = 512;  // pieces per lane and item, their spacing
+constexpr uint32_t kK1LaneBytes = 16;              // (the image's chunk)
+static_assert(kK1Pieces * kK1Piece == 4096 && 32 * kK1LaneBytes == kK1Piece, "K1 covers a 4 KiB item");
+
+struct K1Regs {
+    uint4 d[kK1Pieces];  // piece k: item bytes [512 k + 16 i, +16) for lane i
+    uint32_t cin;        // the item's initial CRC
+    // wb: wave-uniform base (SGPR), loff: this lane's offset from it
+    __device__ __forceinline__ void load_at(const uint8_t *__restrict__ wb, uint32_t loff) {
+#pragma unroll
+        for (int k = 0; k < (int)kK1Pieces; ++k) d[k] = ld16_nt(wb + loff + k * kK1Piece);
+    }
+};
+
+// The lane value M_{2048}(u_A) ^ u_B: u_A / u_B the first / second half's
+// four chains, each ended by its shifted last step.
+__device__ __forceinline__ uint32_t k1_lane_value(const K1Regs &r, const LaneCtx &c) {
+    constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};  // M_1536, M_1024, M_512
+    uint32_t x[kK1Pieces];
+#pragma unroll
+    for (int k = 0; k < (int)kK1Pieces; ++k) x[k] = r.d[k].x;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < (int)kK1Pieces; ++k) x[k] = step4_next(x[k], dw4(r.d[k], i), c);
+#pragma unroll
+    for (int k = 0; k < (int)kK1Pieces; ++k)
+        x[k] = (k & 3) < 3 ? step4_last_shifted(x[k], kShift[k & 3]) : step4_next(x[k], 0u, c);
+    const uint32_t ua = xor3(x[0], x[1], x[2]) ^ x[3], ub = xor3(x[4], x[5], x[6]) ^ x[7];
+    return apply_op<4>(kAuxSpanFold, ua) ^ ub;
+}
+
 template <bool CRCIN>
 __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base, uint64_t stride,
                                                 uint64_t nitems, const uint4 *__restrict__ img,
@@ -113,7 +159,6 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
                                                 uint32_t *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     load_tables(smem, img, kLdsImageK1Bytes);
-    using Regs = ItemRegs<32, kK1CH, kK1Rows>;
     constexpr uint32_t IPW = 2;  // items per wave and step
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t li = lane & 31u;
@@ -144,18 +189,18 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     const uint64_t gend = min((grp + 1) * cg, ngroups);
     grp *= cg;
     if (grp >= ngroups) return;
-    const uint64_t gs = 1, glast = gend - 1;
+    const uint64_t glast = gend - 1;
     auto item_of = [&](uint64_t gi) { return gi * IPW + g; };
 
-    Regs ra, rb;
+    K1Regs ra, rb;
     // Uniform step base + per-lane offset: no 64-bit VGPR address math at the
     // top of a step.  A wave's last prefetch runs one step past its last
-    // group; it re-reads that group (just loaded, cache-hot) -- clamping every
-    // wave to the batch's last group made 4096 waves read the same 8 KiB at
-    // the end of the launch.  The sched_barrier keeps the loads at the top of
-    // the step: left alone, the scheduler sinks them into the chains and the
+    // group; it re-reads that group (just loaded) -- clamping every wave to
+    // the batch's last group made 4096 waves read the same 8 KiB at the end
+    // of the launch.  The sched_barrier keeps the loads at the top of the
+    // step: left alone, the scheduler sinks them into the chains and the
     // next step waits on loads issued moments before.
-    auto ld = [&](Regs &r, uint64_t gi) {
+    auto ld = [&](K1Regs &r, uint64_t gi) {
         const uint64_t gu = gi < gend ? gi : glast;
         const uint64_t first = gu * IPW;
         const uint8_t *wb = base + first * stride;
@@ -165,47 +210,52 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
         // all of its loads before any chain could start)
         if constexpr (CRCIN) r.cin = crc_in[first + gl];
         else r.cin = 0u;
-        r.load_at(wb, gl * (uint32_t)stride + li * kK1CH);
+        r.load_at(wb, gl * (uint32_t)stride + li * kK1LaneBytes);
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto part0 = [&](Regs &m) {
-        if (li == 0) m.d[0][0].x ^= ~m.cin;
-        return reduce_level<0>(lane_partial_x3s<kK1CH>(m, c), (lane & 1u) == 0u);
+    // lane 0 XORs ~crc_in into the item's first dword (a register seeded
+    // with ~crc_in, crc32c.c:166)
+    auto part0 = [&](K1Regs &m) {
+        if (li == 0) m.d[0].x ^= ~m.cin;
+        return reduce_level<0>(k1_lane_value(m, c), (lane & 1u) == 0u);
     };
     // One exit, at the bottom of each loop: a break between the halves would
     // give the loop header a second (un-waited) predecessor, and the waitcnt
     // pass would then drain every prefetched load there.
-    const uint64_t nsteps = (gend - grp + gs - 1) / gs;
+    const uint64_t nsteps = gend - grp;
     ld(ra, grp);
     uint64_t k = 0;
     for (; k + 4 <= nsteps; k += 4) {
-        ld(rb, grp + gs);
+        ld(rb, grp + 1);
         const uint32_t va = part0(ra);
-        ld(ra, grp + 2 * gs);
+        ld(ra, grp + 2);
         const uint32_t vb = part0(rb);
         const uint32_t vab = group_pair_level1(va, vb, lane);
-        ld(rb, grp + 3 * gs);
+        ld(rb, grp + 3);
         const uint32_t vc = part0(ra);
-        ld(ra, grp + 4 * gs);
+        ld(ra, grp + 4);
         const uint32_t vd = part0(rb);
-        const uint32_t raw = group_reduce32_quad(vab, group_pair_level1(vc, vd, lane), lane);
-        const uint64_t item = item_of(grp + (li & 3u) * gs);
+        const uint32_t raw = group_reduce32_quad_span(vab, group_pair_level1(vc, vd, lane), lane);
+        const uint64_t item = item_of(grp + (li & 3u));
         if (li < 4 && item < nitems) out[item] = ~raw;
-        grp += 4 * gs;
+        grp += 4;
     }
     for (; k + 2 <= nsteps; k += 2) {
-        ld(rb, grp + gs);
+        ld(rb, grp + 1);
         const uint32_t va = part0(ra);
-        ld(ra, grp + 2 * gs);
+        ld(ra, grp + 2);
         const uint32_t vb = part0(rb);
-        const uint32_t raw = group_reduce32_pair(va, vb, lane);
-        const uint64_t item = item_of(li == 0 ? grp : grp + gs);
+        const uint32_t raw = group_reduce32_pair_span(va, vb, lane);
+        const uint64_t item = item_of(li == 0 ? grp : grp + 1);
         if (li < 2 && item < nitems) out[item] = ~raw;
-        grp += 2 * gs;
+        grp += 2;
     }
     if (nsteps & 1) {
-        if (li == 0) ra.d[0][0].x ^= ~ra.cin;
-        const uint32_t raw = group_reduce32_dpp(lane_partial_x3s<kK1CH>(ra, c), lane);
+        uint32_t v = part0(ra);
+        v = reduce_level<1>(v, (lane & 3u) == 0u);
+        v = reduce_level<2>(v, (lane & 7u) == 0u);
+        v = reduce_level<3>(v, (lane & 15u) == 0u);
+        const uint32_t raw = reduce_level4_span(v, (lane & 31u) == 0u);
         const uint64_t item = item_of(grp);
         if (li == 0 && item < nitems) out[item] = ~raw;
     }

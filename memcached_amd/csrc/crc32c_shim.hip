@@ -62,8 +62,8 @@ namespace {
 
 constexpr int kBlock = 1024;                    // 16 waves, 32 lane groups
 constexpr uint32_t kItemsPerBlockStep = 32;     // one span per 32-lane group
-constexpr uint32_t kFixedLen = mcrc_dev::kK1Bytes;  // K1: 4 rows x 32 lanes x 32 B
-static_assert(mcrc_dev::kK1CH == mcrc_dev::kSpanCH, "K1 and the span kernels share one table image");
+constexpr uint32_t kFixedLen = mcrc_dev::kK1Bytes;  // K1: 8 pieces x 32 lanes x 16 B
+static_assert(mcrc_dev::kK1CH == mcrc_dev::kSpanCH, "k_small, k_blocks and the span kernels share the row layout");
 
 thread_local float g_last_kernel_ms = -1.0f;
 
@@ -79,7 +79,8 @@ struct Device {
     bool ok = false;
     uint4 *img = nullptr;       // LDS table image of the span kernels (crc32c_gf2.h build_lds_image_span)
     uint32_t *tab8 = nullptr;   // byte-wise table (k_count / k_final: a span's head fragment and foreign bytes)
-    uint4 *img_k1 = nullptr;    // K1 image (160 KiB, crc32c_gf2.h build_lds_image_k1)
+    uint4 *img_k1 = nullptr;    // row image (160 KiB, crc32c_gf2.h build_lds_image_k1): k_small, k_blocks
+    uint4 *img_k1c = nullptr;   // K1 image: build_lds_image_span at chunk 16 (K1's 16-B lane pieces)
     uint32_t *xpow = nullptr;   // x^(8n) table (layout mcrc_dev::kXpow*)
     uint32_t *xk = nullptr;     // k_lines: x^(8e), e in [kXkLo, kXkLo + kXkN)
     uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
@@ -247,6 +248,9 @@ int init_device(Device &d, int id) {
     mcrc::build_lds_image_k1(img_k1.data(), mcrc_dev::kK1CH);
     HIP_OK(hipMalloc(&d.img_k1, img_k1.size() * 4));
     HIP_OK(hipMemcpy(d.img_k1, img_k1.data(), img_k1.size() * 4, hipMemcpyHostToDevice));
+    mcrc::build_lds_image_span(img_k1.data(), mcrc_dev::kK1LaneBytes);
+    HIP_OK(hipMalloc(&d.img_k1c, img_k1.size() * 4));
+    HIP_OK(hipMemcpy(d.img_k1c, img_k1.data(), img_k1.size() * 4, hipMemcpyHostToDevice));
     // rows k (k < kSegpowLo) and kSegpowLo + j (x^(8 * 4096 * kSegpowLo j))
     // for every block shift in a 4 GiB span (a unit's shift: the blocks from
     // its end to the span's end)
@@ -662,25 +666,32 @@ mcrc_dev::SpanArgs span_args(const Device &d, const crc32c_spans &s) {
 // want_host_count (synchronous callers only): a small batch's out-of-range
 // count comes back in d.hbad from k_small itself (no memset, no copy);
 // *host_counted says whether that happened.
+// K1's batch shape: equal 4 KiB spans at a 16-B aligned base and stride (the
+// lane offset within a step, item * stride, is 32-bit in K1).
+bool k1_shape(const crc32c_spans &s) {
+    return s.offsets == nullptr && s.lens == nullptr && s.len == kFixedLen && aligned16(s.base) &&
+           (s.stride & 15u) == 0 && s.stride < (1ull << 31);
+}
+
+// K1 touches no shared scratch, counter or event of the device: callers may
+// enqueue it without d.mu.
+int launch_k1(const Device &d, const crc32c_spans &s, hipStream_t st) {
+    if (s.crc_in)
+        hipLaunchKernelGGL((mcrc_dev::k_fixed<true>), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
+                           st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1c, s.crc_in, s.out);
+    else
+        hipLaunchKernelGGL((mcrc_dev::k_fixed<false>), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
+                           st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1c, s.crc_in, s.out);
+    HIP_OK(hipGetLastError());
+    return CRC32C_OK;
+}
+
 int enqueue_device(Device &d, const crc32c_spans &s, hipStream_t st, bool want_host_count = false,
                    bool *host_counted = nullptr) {
     if (host_counted) *host_counted = false;
     if (s.n == 0) return CRC32C_OK;
     if (!fixed_spans_fit(s)) return CRC32C_EINVAL;
-    const bool fixed = s.offsets == nullptr && s.lens == nullptr;
-    // (the lane offset within a step, item * stride, is 32-bit in K1)
-    if (fixed && s.len == kFixedLen && aligned16(s.base) && (s.stride & 15u) == 0 && s.stride < (1ull << 31)) {
-        if (s.crc_in)
-            hipLaunchKernelGGL((mcrc_dev::k_fixed<true>), dim3(grid_for(d, s.n)), dim3(kBlock),
-                               mcrc_dev::kLdsImageK1Bytes, st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1,
-                               s.crc_in, s.out);
-        else
-            hipLaunchKernelGGL((mcrc_dev::k_fixed<false>), dim3(grid_for(d, s.n)), dim3(kBlock),
-                               mcrc_dev::kLdsImageK1Bytes, st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1,
-                               s.crc_in, s.out);
-        HIP_OK(hipGetLastError());
-        return CRC32C_OK;
-    }
+    if (k1_shape(s)) return launch_k1(d, s, st);
     const mcrc_dev::SpanArgs a = span_args(d, s);
     Path path;
     path.small = takes_small<0>(a);
@@ -916,6 +927,10 @@ int run_host_batch(Device &d, const crc32c_spans &s) {
 // buffer.
 int device_batch(Device &d, const crc32c_spans &s, unsigned flags, hipStream_t st) {
     if (s.n && !device_range_ok(s.base, s.base_bytes)) return CRC32C_EINVAL;
+    // an asynchronous K1 batch needs nothing the lock guards (no scratch, no
+    // timing events): IO or device threads enqueue it concurrently
+    if ((flags & CRC32C_ASYNC) && s.n && k1_shape(s))
+        return fixed_spans_fit(s) ? launch_k1(d, s, st) : CRC32C_EINVAL;
     std::lock_guard<std::mutex> lk(d.mu);
     const bool timed = !(flags & CRC32C_ASYNC);
     d.acquire(st);

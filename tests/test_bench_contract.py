@@ -26,12 +26,15 @@ def test_traffic_is_the_k_fixed_record_of_the_batch_shape():
 def test_traffic_record_selection(tmp_path, monkeypatch):
     prof = tmp_path / "profiles"
     prof.mkdir()
-    rec = {"kernel": "k_fixed", "items": 1 << 20, "item_bytes": 4096, "hbm_bytes_per_launch": 111.0}
+    rec = {"kernel": "k_fixed", "k1_layout": bench.K1_LAYOUT, "items": 1 << 20, "item_bytes": 4096,
+           "hbm_bytes_per_launch": 111.0}
     (prof / "r01_traffic.json").write_text(json.dumps(dict(rec, hbm_bytes_per_launch=100.0)))
     (prof / "r02_traffic.json").write_text(json.dumps(rec))
     (prof / "r02_traffic_spans.json").write_text(json.dumps({"config3": {"traffic_over_algorithmic": 1.02}}))
     (prof / "r03_traffic_other.json").write_text(json.dumps(dict(rec, kernel="k_spans", hbm_bytes_per_launch=9.0)))
     (prof / "r04_traffic_broken.json").write_text("{not json")
+    # (a newer record of the earlier K1 layout is not this K1's traffic)
+    (prof / "r05_traffic_old_k1.json").write_text(json.dumps(dict(rec, k1_layout="rows32", hbm_bytes_per_launch=5.0)))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
     assert bench.traffic_per_launch(1 << 20, 4096) == 111.0
     assert bench.traffic_per_launch(1 << 19, 4096) is None

@@ -11,6 +11,8 @@ import json
 import sys
 from collections import defaultdict
 
+K1_LAYOUT = "pieces16-nt"  # = bench.K1_LAYOUT (the K1 load shape the record measures)
+
 
 def per_dispatch(path, counter, kernel_substr):
     vals = defaultdict(float)
@@ -35,6 +37,8 @@ def main(fetch_dir, write_dir, out, kernel="k_fixed", items=1 << 20, item_bytes=
         "traffic_over_algorithmic": (fetch + write) / (items * item_bytes),
         "correction": "FETCH_SIZE x 2 (gfx950), WRITE_SIZE x 1, KiB -> bytes",
     }
+    if kernel == "k_fixed":
+        rec["k1_layout"] = K1_LAYOUT
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec))
 
