@@ -47,6 +47,10 @@ __device__ __forceinline__ uint4 ld16_nt(const uint8_t *p) {
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+__device__ __forceinline__ uint4 ld16_nt(gbyte *p) {
+    const u32x4 v = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4 *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 __device__ __forceinline__ uint32_t dw4(const uint4 &v, int k) {
     return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
@@ -1809,8 +1813,8 @@ constexpr uint32_t kStFused = 0x10u, kStSane = 0x20u, kStValid = 0x40u;
 constexpr uint32_t kEpoch = 32;                                 // steps per epoch: 64 images per wave
 
 struct ItemBuf {
-    ItemRegs<32, 32, 4> d;  // the block, rows 0..3
-    uint32_t st;            // its image: t | kStFused | kStSane | kStValid
+    K1Regs d;     // the window, in K1's lane layout (pieces 512 k + 16 li)
+    uint32_t st;  // its image: t | kStFused | kStSane | kStValid
 };
 
 // ===========================================================================
@@ -1991,22 +1995,25 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
         r_t = p_nt ? step4_next(x, 0u, c) : 0u;
     };
     // Loads of step s (< ns, else a repeat of the run's last step, whose
-    // result is not used) into b: its window and its status.
+    // result is not used) into b: its window and its status.  K1's layout
+    // and policy (round 5): lane li holds the window's 16-B pieces at
+    // 512 k + 16 li, each instruction reads whole lines, non-temporal (the
+    // window's lines are read by nothing else: the heads and tails lie
+    // outside [A, B)): config 2r 0.743-0.766 -> 0.693-0.694 ms, config 5
+    // 3.58-3.59 -> 3.50 ms and stamp 3.85-3.86 -> 3.75-3.76 ms per 300 pages
+    // (profiles/r05_ablations/k5_lines_pieces_nt_ab.txt).
     auto ld = [&](ItemBuf &b, uint32_t s, uint32_t ns) {
         const int src = (int)(2 * min(s, ns - 1) + g);
         const uint64_t lo = (uint32_t)__shfl((int)eglo, src, 64), hi = (uint32_t)__shfl((int)eghi, src, 64);
         b.st = (uint32_t)__shfl((int)est, src, 64);
-        gbyte *blk = (b.st & kStFused) ? gb + (lo | (hi << 32)) : gz;
-        const bool z3 = (b.st & kSt31) && li >= 28u;  // row 3 past B: zeros
+        gbyte *blk = ((b.st & kStFused) ? gb + (lo | (hi << 32)) : gz) + 16 * li;
+        const bool z7 = (b.st & kSt31) && li >= 24u;  // piece 7 past B (the window's last line): zeros
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-            for (int q = 0; q < 2; ++q) b.d.d[r][q] = ld16(blk + r * 1024 + li * 32 + 16 * q);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) b.d.d[3][q] = ld16(z3 ? gz + 16 * q : blk + 3072 + li * 32 + 16 * q);
+        for (int k = 0; k < (int)kK1Pieces - 1; ++k) b.d.d[k] = ld16_nt(blk + k * kK1Piece);
+        b.d.d[kK1Pieces - 1] = ld16_nt(z7 ? gz + 16 * li : blk + (kK1Pieces - 1) * kK1Piece);
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto part0 = [&](ItemBuf &b) { return reduce_level<0>(lane_partial_x3s<32>(b.d, c), (lane & 1u) == 0u); };
+    auto part0 = [&](ItemBuf &b) { return reduce_level<0>(k1_lane_value(b.d, c), (lane & 1u) == 0u); };
     // The epoch lanes collect R of their images from the lanes that finished
     // them (steps s0 .. s0 + cnt - 1 in lanes 0 .. cnt - 1 of each group).
     auto collect = [&](uint32_t r, uint32_t s0, uint32_t cnt) {

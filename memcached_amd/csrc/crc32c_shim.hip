@@ -432,7 +432,7 @@ void launch_k5(const Device &d, const mcrc_dev::SpanArgs &a, mcrc_dev::ItemsOut 
     io.xk = d.xk;
     io.nsr = (uint32_t)std::min<uint64_t>(mcrc_dev::kEpoch, std::max<uint64_t>(1, (a.n + 2 * waves - 1) / (2 * waves)));
     hipLaunchKernelGGL((mcrc_dev::k_lines<MODE, OFFS>), dim3(grid), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st, a,
-                       d.img, io);
+                       d.img_k1c, io);
 }
 
 // Large item batches go through launch_items, where k_census samples their
