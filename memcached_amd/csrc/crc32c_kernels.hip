@@ -1226,7 +1226,7 @@ __device__ __forceinline__ PlanSum plan_at(const uint64_t *nunit, const uint8_t 
     return i < n ? plan_of(nunit[i], fast[i]) : PlanSum{0, 0, 0, 0};
 }
 
-// Tile t's sum (thread-contiguous: thread k holds spans t*kPlanTile + 8k .. +7).
+// Tile t's sum (thread-contiguous: thread k holds spans t*kPlanTile + kPlanPer k .. + kPlanPer - 1).
 __global__ __launch_bounds__(kPlanThreads) void k_plan_tiles(const uint64_t *nunit, const uint8_t *fast, uint64_t n,
                                                             const uint32_t *dn, PlanSum *tile_sum) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
