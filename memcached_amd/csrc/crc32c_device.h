@@ -1,28 +1,31 @@
 // crc32c_device.h -- CDNA4 (gfx950) device primitives for batched CRC-32C.
 //
 // Work model.  A 32-lane group owns one item span (a wavefront holds two).
-// The span is cut into 4 KiB blocks of four 1 KiB rows; lane i of the group
-// owns bytes [32 i, 32 i + 32) of every row and runs one table-driven chain
-// per row.  The lane partials of a group are merged by a 5-level reduction
-// whose level k applies the fixed zeros operator M_{32 * 2^k}.  This is the
-// algebra the reference uses to merge its three crc32q streams
-// (crc32c.c:184-220, zeros operators crc32c.c:85-137), widened from 3 streams
-// to 128 per 4 KiB.
+// The span is cut into 4 KiB blocks; lane i of the group holds the 16-B
+// pieces at 512 k + 16 i of a block (k = 0..7: each load instruction reads
+// 512 contiguous bytes per group) and runs one table-driven chain per piece.
+// The chains of each 2 KiB half fold through shifted last-step tables, the
+// first half moves up by M_2048, and the lane values of a group merge in a
+// 5-level reduction whose level k applies the fixed zeros operator
+// M_{16 * 2^k}.  This is the algebra the reference uses to merge its three
+// crc32q streams (crc32c.c:184-220, zeros operators crc32c.c:85-137), widened
+// from 3 streams to 256 per 4 KiB.
 //
 // Tables live in LDS.  The slice-by-4 tables are replicated once per bank of a
 // 32-lane bank group so every data lookup is conflict-free (lane l always
-// reads bank l % 32); the 160 KiB image (crc32c_gf2.h build_lds_image4/_k1):
+// reads bank l % 32); the 160 KiB image (crc32c_gf2.h build_lds_image_span at
+// chunk 16, one image for every kernel since round 5):
 //   [0, 28 KiB)          aux tables, plain: table t entry e at t*1024 + e*4
 //   [28 KiB, +64 KiB)    row e: T3[e] x 32 | T2[e] x 32
 //   [92 KiB, +64 KiB)    row e: T1[e] x 32 | T0[e] x 32
-//   [156 KiB, 160 KiB)   K1: four more aux tables (row 0's shifted last step)
+//   [156 KiB, 160 KiB)   four more aux tables (the M_1536 shifted last step)
 // where Tk[b] = register after byte b then k zero bytes (crc32c.c:366-389).
 //
 // Aux tables hold the byte slices of zeros operators (crc32c.c:121-137 form);
 // operator o occupies aux tables 4o..4o+3:
-//   o = 0..4 : M_{32 * 2^o}  (lane-group reduction level o)
-//   o = 5, 6 : K1: the shifted last-step tables of rows 2 and 1
-//   span image: o = 4 is the 4 KiB block fold (level 4 = level 3 twice)
+//   o = 0..3 : M_{16 * 2^o}  (lane-group reduction level o; level 4 = level 3 twice)
+//   o = 4    : M_2048, the half-block fold (kAuxSpanFold)
+//   o = 5, 6 : the shifted last steps M_512, M_1024 (tables 156..159: M_1536)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -85,8 +88,9 @@ __device__ __forceinline__ uint32_t step4_next(uint32_t x, uint32_t w_next, cons
     return xor3(xor3(a3, a2, a1), a0, w_next);
 }
 
-// K1 image (crc32c_gf2.h build_lds_image_k1): last-step tables of row chains
-// 0, 1, 2 with the row fold M_{(3-r)*1024} applied (4 plain tables each).
+// Shifted last-step tables (crc32c_gf2.h build_lds_image_k1 at chunk 16):
+// pieces 0, 1, 2 of each half with their fold M_{(3-k)*512} applied (4 plain
+// tables each).
 constexpr uint32_t kAuxShift0 = 156, kAuxShift1 = 24, kAuxShift2 = 20;
 constexpr uint32_t kLdsImageK1Bytes = 160 * 1024;
 
@@ -117,21 +121,6 @@ __device__ __forceinline__ uint32_t lane_down(uint32_t v) {
     }
 }
 
-// group_reduce for LPI = 32 with DPP / permlane lane moves (slice-by-4 aux).
-template <int K = 0>
-__device__ __forceinline__ uint32_t group_reduce32_dpp(uint32_t v, uint32_t lane) {
-    if constexpr (K == 5) {
-        return v;
-    } else {
-        const uint32_t x = lane_down<K>(v);
-        if ((lane & ((2u << K) - 1u)) == 0) v = xor3(Step<4>::aux(kAuxTree + 4 * K, v & 0xffu) ^ x,
-                                                      Step<4>::aux(kAuxTree + 4 * K + 1, (v >> 8) & 0xffu),
-                                                      Step<4>::aux(kAuxTree + 4 * K + 2, (v >> 16) & 0xffu)) ^
-                                                 Step<4>::aux(kAuxTree + 4 * K + 3, v >> 24);
-        return group_reduce32_dpp<K + 1>(v, lane);
-    }
-}
-
 // One level of the LPI = 32 reduction on the lanes selected by `on`.
 template <int K>
 __device__ __forceinline__ uint32_t reduce_level(uint32_t v, bool on) {
@@ -142,21 +131,6 @@ __device__ __forceinline__ uint32_t reduce_level(uint32_t v, bool on) {
     return v;
 }
 
-// Reduction of two items per 32-lane group (two consecutive steps of K1): a
-// holds item A's level-0 results on even lanes, b item B's on even lanes.
-// B's are moved to the odd lanes (DPP row_shr:1) and levels 1..4 run once for
-// both: at level k the lanes l with l % 2^(k+1) in {0, 1} merge with lane
-// l + 2^k, so A's raw CRC ends in lane 0 and B's in lane 1 of the group.
-// Saves four of the five levels of the second item's reduction.
-__device__ __forceinline__ uint32_t group_reduce32_pair(uint32_t a, uint32_t b, uint32_t lane) {
-    const uint32_t bs = __builtin_amdgcn_update_dpp(0u, b, 0x111, 0xf, 0xf, false);  // row_shr:1
-    uint32_t v = (lane & 1u) ? bs : a;
-    v = reduce_level<1>(v, (lane & 3u) < 2u);
-    v = reduce_level<2>(v, (lane & 7u) < 2u);
-    v = reduce_level<3>(v, (lane & 15u) < 2u);
-    return reduce_level<4>(v, (lane & 31u) < 2u);
-}
-
 // Level 1 of two items' reductions (A on lanes 0 mod 4, B on lanes 1 mod 4
 // afterwards), for group_reduce32_quad.
 __device__ __forceinline__ uint32_t group_pair_level1(uint32_t a, uint32_t b, uint32_t lane) {
@@ -164,23 +138,12 @@ __device__ __forceinline__ uint32_t group_pair_level1(uint32_t a, uint32_t b, ui
     return reduce_level<1>((lane & 1u) ? bs : a, (lane & 3u) < 2u);
 }
 
-// Four items per 32-lane group: ab and cd from group_pair_level1; cd moves up
-// two lanes (DPP row_shr:2) and levels 2..4 run once for all four, so items
-// A, B, C, D end in lanes 0, 1, 2, 3 of the group.
-__device__ __forceinline__ uint32_t group_reduce32_quad(uint32_t ab, uint32_t cd, uint32_t lane) {
-    const uint32_t cs = __builtin_amdgcn_update_dpp(0u, cd, 0x112, 0xf, 0xf, false);  // row_shr:2
-    uint32_t v = (lane & 2u) ? cs : ab;
-    v = reduce_level<2>(v, (lane & 7u) < 4u);
-    v = reduce_level<3>(v, (lane & 15u) < 4u);
-    return reduce_level<4>(v, (lane & 31u) < 4u);
-}
-
-// Span image (crc32c_gf2.h build_lds_image_span): aux tables 16..19 hold the
-// 4 KiB block fold instead of tree level 4.
+// Aux tables 16..19 hold the half-block fold M_2048 (build_lds_image_span at
+// chunk 16: M_{128 chunk}) instead of tree level 4.
 constexpr uint32_t kAuxSpanFold = 16;
 
-// group_reduce32_dpp on the span image: level 4 (M_512) is level 3 (M_256)
-// applied twice.
+// The full five-level reduction of a group's lane values into lane 0: level
+// 4 (M_256) is level 3 (M_128) applied twice.
 __device__ __forceinline__ uint32_t group_reduce32_span(uint32_t v, uint32_t lane) {
     v = reduce_level<0>(v, (lane & 1u) == 0u);
     v = reduce_level<1>(v, (lane & 3u) == 0u);
@@ -191,8 +154,8 @@ __device__ __forceinline__ uint32_t group_reduce32_span(uint32_t v, uint32_t lan
     return v;
 }
 
-// The pair / quad reductions on the span image (level 4 = level 3 twice, its
-// tables 16..19 hold the 4 KiB block fold).
+// Level 4 as level 3 twice (tables 16..19 hold the half-block fold), and the
+// pair / quad reductions of two or four items per group.
 __device__ __forceinline__ uint32_t reduce_level4_span(uint32_t v, bool on) {
     const uint32_t x = lane_down<4>(v);
     if (on) v = apply_op<4>(kAuxTree + 12, apply_op<4>(kAuxTree + 12, v)) ^ x;

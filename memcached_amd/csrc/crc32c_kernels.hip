@@ -56,58 +56,9 @@ __device__ __forceinline__ uint32_t dw4(const uint4 &v, int k) {
     return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
 }
 
-// One lane's share of one item: R rows x CH bytes, 16-B loads.
-template <int LPI, int CH, int R>
-struct ItemRegs {
-    static constexpr int Q = CH / 16;
-    uint4 d[R][Q];
-    uint32_t cin;  // the item's initial CRC
-
-    __device__ __forceinline__ void load(const uint8_t *__restrict__ p, uint32_t li) {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int q = 0; q < Q; ++q)
-                d[r][q] = ld16(p + (size_t)r * LPI * CH + li * CH + 16 * q);
-    }
-    // wb: wave-uniform base (SGPR), loff: this lane's byte offset from it
-    __device__ __forceinline__ void load_at(const uint8_t *__restrict__ wb, uint32_t loff) {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int q = 0; q < Q; ++q) d[r][q] = ld16(wb + loff + (r * LPI * CH + 16 * q));
-    }
-};
-
-// Lane partial of a 32-lane group on the K1 image: four row chains (slice-by-4,
-// interleaved dword by dword for ILP, two v_bitop3 per step); the last step of
-// row chains 0..2 reads the shifted tables (the row fold M_{(3-r)*1024}
-// included), so the lane partial is the XOR of the four chains.
-template <int CH>
-__device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &it, const LaneCtx &c) {
-    constexpr int Q = CH / 16;
-    constexpr int N = 4 * Q;  // dwords per chain
-    constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};
-    uint32_t x[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) x[r] = it.d[r][0].x;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (i + 1 < N) {
-                x[r] = step4_next(x[r], dw4(it.d[r][(i + 1) >> 2], (i + 1) & 3), c);
-            } else {
-                x[r] = r < 3 ? step4_last_shifted(x[r], kShift[r]) : step4_next(x[r], 0u, c);
-            }
-        }
-    }
-    return xor3(x[0], x[1], x[2]) ^ x[3];
-}
-
-// K1 geometry: a 32-lane group owns one 4096-B item (4 rows of 1 KiB, lane i
-// owns bytes [32 i, 32 i + 32) of each row), a wave two items per step.
-constexpr uint32_t kK1Rows = 4, kK1CH = 32, kK1Bytes = kK1Rows * 32 * kK1CH;  // (the row layout: k_lines)
+// K1 geometry: a 32-lane group owns one 4096-B item, a wave two items per
+// step.
+constexpr uint32_t kK1Bytes = 4096;
 
 // K1's lane layout (round 5).  A 32-lane group owns one 4096-B item, and lane
 // i holds the 16-B pieces at 512 k + 16 i, k = 0..7: each load instruction
@@ -132,9 +83,14 @@ struct K1Regs {
     uint4 d[kK1Pieces];  // piece k: item bytes [512 k + 16 i, +16) for lane i
     uint32_t cin;        // the item's initial CRC
     // wb: wave-uniform base (SGPR), loff: this lane's offset from it
+    // NT: the non-temporal policy, for whole-line (128-B aligned) items; a
+    // 16-B anchored block shares its end lines with its neighbours, which a
+    // non-temporal load fetches twice
+    template <bool NT>
     __device__ __forceinline__ void load_at(const uint8_t *__restrict__ wb, uint32_t loff) {
 #pragma unroll
-        for (int k = 0; k < (int)kK1Pieces; ++k) d[k] = ld16_nt(wb + loff + k * kK1Piece);
+        for (int k = 0; k < (int)kK1Pieces; ++k)
+            d[k] = NT ? ld16_nt(wb + loff + k * kK1Piece) : ld16(wb + loff + k * kK1Piece);
     }
 };
 
@@ -214,7 +170,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
         // all of its loads before any chain could start)
         if constexpr (CRCIN) r.cin = crc_in[first + gl];
         else r.cin = 0u;
-        r.load_at(wb, gl * (uint32_t)stride + li * kK1LaneBytes);
+        r.template load_at<true>(wb, gl * (uint32_t)stride + li * kK1LaneBytes);
         __builtin_amdgcn_sched_barrier(0);
     };
     // lane 0 XORs ~crc_in into the item's first dword (a register seeded
@@ -270,7 +226,8 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 // ===========================================================================
 //
 // Pieces as they lie.  A span D = [p, E) is read as the 16-B aligned pieces
-// [ph, Ea), ph = p rounded down and Ea = E rounded up to 16 (tail_pad),
+// [ph, Ea), ph = p rounded down to 16 and Ea = E rounded up to a 128-B line
+// (grid_pad, round 5; 16 before),
 // foreign bytes included: the span kernel computes R = raw([ph, Ea)) with no
 // masking and no initial value.  With F_h = [ph, p), F_t = [E, Ea),
 // t = |F_t|, the algebra of crc32c.c:58-137 gives
@@ -305,8 +262,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 // pages holding the span); a piece wholly outside is read from a zeroed device
 // buffer instead, so no load is predicated.
 
-constexpr uint32_t kSpanCH = 32;
-constexpr uint32_t kRowBytes = 32 * kSpanCH;  // 1024
+constexpr uint32_t kRowBytes = 1024;  // a row: two of K1's 512-B piece rows (the head-block skip)
 constexpr uint32_t kBlockBytes = 4 * kRowBytes;  // 4096
 constexpr uint32_t kSegBytes = 64 * 1024;  // (16-256 KiB measured; 24-64 KiB alike)
 // Longest span (CRC32C_MAX_SPAN): a unit's grid offsets (eo, G - p, the block
@@ -386,6 +342,14 @@ constexpr uint32_t kTailAlign = 16;
 __device__ __forceinline__ uint32_t tail_pad(const uint8_t *p, uint32_t len) {
     return (uint32_t)(-(uintptr_t)(p + len)) & (kTailAlign - 1);
 }
+// The planned path's grid (round 5): anchored at Ea = E rounded up to a
+// 128-B line, so every block of a unit is whole lines and the span kernel's
+// non-temporal loads never share a line between two instructions; the
+// span's thread folds up to 127 foreign tail bytes instead of 15.
+constexpr uint32_t kGridAlign = 128;
+__device__ __forceinline__ uint32_t grid_pad(const uint8_t *p, uint32_t len) {
+    return (uint32_t)(-(uintptr_t)(p + len)) & (kGridAlign - 1);
+}
 
 // Segments of a virtual span of vlen bytes, anchored at Ea; the head segment
 // keeps the remainder (17 B up to kSegBytes + 16 B).
@@ -394,8 +358,8 @@ __device__ __forceinline__ uint32_t nseg_of(uint32_t vlen) {
 }
 
 // Layout of the x^(8n) table (SpanArgs::xpow).
-constexpr uint32_t kXpowInv = 3072;                // x^(-8t), t < kTailAlign
-constexpr uint32_t kXpowL3 = kXpowInv + kTailAlign;  // x^(8 * 2^30 * j), j < 8
+constexpr uint32_t kXpowInv = 3072;                // x^(-8t), t < kGridAlign
+constexpr uint32_t kXpowL3 = kXpowInv + kGridAlign;  // x^(8 * 2^30 * j), j < 8
 constexpr uint32_t kXpowDwords = kXpowL3 + 8;
 
 // x^(8n) mod P (n < 2^33): one to four table entries multiplied.
@@ -525,7 +489,7 @@ __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, ui
 // DESIGN.md section 3.)
 constexpr uint32_t kFragMax = 128;    // a head fragment [p, G1) of at most this
 constexpr uint32_t kWholeMax = 1024;  // a whole span of vlen at most this
-static_assert(kWholeMax + 16 <= kBlockBytes, "a whole span held by its thread is its own fragment (G1 = Ea)");
+static_assert(kWholeMax + kGridAlign <= kBlockBytes, "a whole span held by its thread is its own fragment (G1 = Ea)");
 // Is the head fragment (G1 - p = g1o) the span thread's?  For vlen <= kWholeMax
 // the fragment is the whole span (G1 = Ea).
 __device__ __forceinline__ bool frag_drop(uint32_t len, uint64_t g1o, uint64_t vlen) {
@@ -537,7 +501,7 @@ struct SpanHead {
 };
 __device__ __forceinline__ SpanHead span_head(const uint8_t *p, uint32_t len) {
     const uint64_t kh = (uintptr_t)p & 15u;
-    const uint64_t x = (uint64_t)len + tail_pad(p, len) + kh;  // Ea - ph
+    const uint64_t x = (uint64_t)len + grid_pad(p, len) + kh;  // Ea - ph
     const uint64_t g1o = x - kBlockBytes * ((x - 1) / kBlockBytes) - kh;
     return {g1o, frag_drop(len, g1o, x - kh)};
 }
@@ -547,7 +511,7 @@ __device__ __forceinline__ SpanHead span_head(const uint8_t *p, uint32_t len) {
 // or it has no unit at all (*none); false: neither.
 __device__ __forceinline__ bool one_block(const uint8_t *p, uint32_t len, const uint8_t **g1, bool *none) {
     const uint64_t kh = (uintptr_t)p & 15u;
-    const uint64_t vlen = (uint64_t)len + tail_pad(p, len);  // (64-bit: len may be close to 2^32)
+    const uint64_t vlen = (uint64_t)len + grid_pad(p, len);  // (64-bit: len may be close to 2^32)
     const uint64_t x = vlen + kh;  // Ea - ph
     const uint64_t g1o = x - kBlockBytes * ((x - 1) / kBlockBytes) - kh;
     const bool drop = frag_drop(len, g1o, vlen);
@@ -574,7 +538,7 @@ __device__ __forceinline__ bool one_block(const uint8_t *p, uint32_t len, const 
 // case above; also k_count's wave-cooperative whole spans, whole_chunks).
 __device__ __forceinline__ uint32_t span_corr_pieces(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
                                                      const uint32_t *xp) {
-    const uint32_t t = tail_pad(p, len);
+    const uint32_t t = grid_pad(p, len);
     const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
     uint32_t y = ~c;
     if (kh) y ^= raw16(shl_bytes(ld_piece(p - kh), 16 - kh), t8);  // raw(F_h)
@@ -584,11 +548,11 @@ __device__ __forceinline__ uint32_t span_corr_pieces(const uint8_t *p, uint32_t 
 }
 __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
                                               const uint32_t *xp) {
-    const uint32_t t = tail_pad(p, len);
-    if (len == 0) return t8.zeros(~c, t);
+    const uint32_t t = grid_pad(p, len);
+    if (len == 0) return mulmodp_dev(~c, xp[t]);
     const uint64_t vlen = (uint64_t)len + t;
     const SpanHead h = span_head(p, len);
-    if (h.drop && h.g1o == vlen) return t8.zeros(reg_advance(~c, p, len, t8), t);
+    if (h.drop && h.g1o == vlen) return mulmodp_dev(reg_advance(~c, p, len, t8), xp[t]);
     if (!h.drop) return span_corr_pieces(p, len, c, t8, xp);
     // Ea - G1 is whole blocks; one block (every one-block span) is a table step
     const uint32_t r = reg_advance(~c, p, (uint32_t)h.g1o, t8);
@@ -697,7 +661,7 @@ struct UnitDesc {
 __device__ __forceinline__ UnitRec make_unit(const uint8_t *base, uint64_t off, uint32_t len, uint32_t aux,
                                              bool sane, uint32_t item, uint32_t seg) {
     const uint8_t *p0 = base + off;
-    const uint32_t vlen = len + tail_pad(p0, len);
+    const uint32_t vlen = len + grid_pad(p0, len);
     const uint32_t nseg = seg == kWhole ? 1u : nseg_of(vlen);
     const bool single = nseg == 1, head = single || seg == 0;
     const uint32_t eo0 = vlen - (single ? 0u : (nseg - 1 - seg) * kSegBytes);  // e - p0
@@ -774,7 +738,7 @@ __device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw,
         const bool sane = off <= a.base_bytes && a.len <= a.base_bytes - off;  // else: read nothing
         const uint32_t len = sane ? a.len : 0u;
         const uint32_t plo = (uint32_t)(uintptr_t)a.base + (uint32_t)off, kh = plo & 15u;
-        const uint32_t vlen = len + ((0u - plo - len) & (kTailAlign - 1));  // tail_pad
+        const uint32_t vlen = len + ((0u - plo - len) & (kGridAlign - 1));  // grid_pad
         const uint32_t x = vlen + kh;  // Ea - ph
         const uint32_t g1o = x - kBlockBytes * ((x - 1) >> 12) - kh;  // span_head
         const uint32_t po = frag_drop(len, g1o, vlen) ? g1o : 0u;
@@ -787,59 +751,72 @@ __device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw,
     return d;
 }
 
+// (non-temporal: the planned path's blocks are whole lines since round 5,
+// kGridAlign; config 3 -1.5 to -2 %, mixed pages -1.3 % against the row
+// layout, profiles/r05_ablations/spans_line_grid_ab.txt)
+constexpr bool kSpanNT = true;
+// A 4 KiB block of a unit in K1's lane layout (round 5): lane li holds the
+// 16-B pieces at G + 512 k + 16 li, k = 0..7, so each load instruction reads
+// 512 contiguous bytes per group, non-temporal (crc32c_kernels.hip K1).
 struct BlockWin {
-    uint4 v[4][2];  // [row][piece]
+    uint4 v[kK1Pieces];
 };
 
 // Issue the loads of block k of unit d for lane li.
 __device__ __forceinline__ void load_block(BlockWin &w, const UnitDesc &d, uint32_t k, uint32_t li,
                                            const uint4 *zero) {
     // Offsets relative to the unit's first byte p: block start G - p = grel;
-    // lane li's row-r chunk is [grel + 1024 r + 32 li, +32), its pieces at +0
-    // and +16.  A piece that ends at or before ph = floor16(p) reads the zero
-    // line (only head blocks have such pieces); every other piece overlaps
-    // [ph, e), so no load leaves the pages of the span.  zl points 16 bytes
-    // into this workgroup's zero line, so zl and zl + 16 are both zeros.
+    // lane li's piece k is [grel + 512 k + 16 li, +16).  A piece that ends at
+    // or before ph = floor16(p) reads the zero line (only head blocks have
+    // such pieces); every other piece overlaps [ph, e), so no load leaves the
+    // pages of the span.
     const int32_t grel = (int32_t)d.eo - (int32_t)(kBlockBytes * (d.niters() - k));
-    const int32_t lrel = grel + (int32_t)(kSpanCH * li);
+    const int32_t lrel = grel + (int32_t)(kK1LaneBytes * li);
     const uint8_t *q0 = d.p + lrel;
-    const uint8_t *zl = reinterpret_cast<const uint8_t *>(zero) + 16;
-    // piece-0 end - ph, row 0; a unit without blocks (no bytes, or no unit)
-    // reads nothing but zeros
+    const uint8_t *zl = reinterpret_cast<const uint8_t *>(zero);
+    // piece-0 end - ph; a unit without blocks (no bytes, or no unit) reads
+    // nothing but zeros
     const int32_t e0 = d.niters() ? lrel + 16 + (int32_t)((uintptr_t)d.p & 15u) : -(int32_t)kBlockBytes - 16;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint8_t *rb = q0 + r * kRowBytes;
-        const int32_t er = e0 + r * (int32_t)kRowBytes;
-        w.v[r][0] = ld16(er > 0 ? rb : zl);
-        w.v[r][1] = ld16((er + 16 > 0 ? rb : zl) + 16);
+    for (int j = 0; j < (int)kK1Pieces; ++j) {
+        const uint8_t *q = e0 + j * (int32_t)kK1Piece > 0 ? q0 + j * kK1Piece : zl;
+        w.v[j] = kSpanNT ? ld16_nt(q) : ld16(q);
     }
 }
 
-// Chains over rows NS..3 of a block, as in K1: the last step of rows 0-2
-// reads the shifted tables of the span image (row fold included), so the
-// block's lane value is the XOR of the chains.
-template <int NS>
-__device__ __forceinline__ uint32_t block_value(const BlockWin &w, const LaneCtx &c) {
+// acc' = M_4096(acc) ^ (the block's lane value) = M_2048(M_2048(acc) ^ u_A) ^ u_B
+// (u_A / u_B: the first / second half's chains, k1_lane_value; M_2048 = the
+// chunk-16 image's tables 16..19).  NS: rows (piece pairs) 0..NS-1 lie wholly
+// before p for every lane of the wave (their chains are of zeros and are
+// skipped); fold: some group of the wave is past its unit's first block
+// (wave-uniform; else every acc is 0 and is not folded).
+// The chains of one half's pieces v[J0..3] (v[j] for j < J0 are zeros and
+// are skipped), each ended by its shifted last step: the half's value.  (One
+// half at a time: eight live chains beside the prefetched block pushed the
+// span kernel past 128 VGPRs into scratch.)
+template <int J0>
+__device__ __forceinline__ uint32_t half_value(const uint4 *v, const LaneCtx &c) {
     constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};
     uint32_t x[4];
 #pragma unroll
-    for (int r = NS; r < 4; ++r) x[r] = w.v[r][0].x;
+    for (int j = J0; j < 4; ++j) x[j] = v[j].x;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 1; i < 4; ++i)
 #pragma unroll
-        for (int r = NS; r < 4; ++r) {
-            if (i + 1 < 8) {
-                x[r] = step4_next(x[r], dw4(w.v[r][(i + 1) >> 2], (i + 1) & 3), c);
-            } else {
-                x[r] = r < 3 ? step4_last_shifted(x[r], kShift[r]) : step4_next(x[r], 0u, c);
-            }
-        }
-    }
-    uint32_t v = x[3];
+        for (int j = J0; j < 4; ++j) x[j] = step4_next(x[j], dw4(v[j], i), c);
+    uint32_t u = 0;
 #pragma unroll
-    for (int r = NS; r < 3; ++r) v ^= x[r];
-    return v;
+    for (int j = J0; j < 4; ++j) u ^= j < 3 ? step4_last_shifted(x[j], kShift[j]) : step4_next(x[j], 0u, c);
+    return u;
+}
+
+template <int NS>
+__device__ __forceinline__ uint32_t block_fold(uint32_t acc, bool fold, const BlockWin &w, const LaneCtx &c) {
+    const uint32_t ub = half_value<NS == 3 ? 2 : 0>(w.v + 4, c);
+    if (NS >= 2 && !fold) return ub;
+    uint32_t h = fold ? apply_op<4>(kAuxSpanFold, acc) : 0u;
+    if (NS < 2) h ^= half_value<2 * (NS & 1)>(w.v, c);
+    return apply_op<4>(kAuxSpanFold, h) ^ ub;
 }
 
 // Store (MODE 0) or stamp (MODE 2) the CRC of span `item`, which starts at p.
@@ -968,10 +945,8 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         // pending in the waitcnt pass's view, and the next write to those
         // registers became an s_waitcnt vmcnt(0) that drained the prefetch).
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                asm volatile("" ::"v"(w.v[r][q].x), "v"(w.v[r][q].y), "v"(w.v[r][q].z), "v"(w.v[r][q].w));
+        for (int j = 0; j < (int)kK1Pieces; ++j)
+            asm volatile("" ::"v"(w.v[j].x), "v"(w.v[j].y), "v"(w.v[j].z), "v"(w.v[j].w));
         if (cur.niters()) {
             const int32_t grel = (int32_t)cur.eo - (int32_t)(kBlockBytes * (cur.niters() - k));  // G - p
             // rows wholly before p for every lane of the wave are skipped
@@ -980,17 +955,15 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
                                    : __all(grel + 2 * (int32_t)kRowBytes <= 0) ? 2u
                                    : __all(grel + (int32_t)kRowBytes <= 0)     ? 1u
                                                                                : 0u;
-            uint32_t v;
-            switch (nskip) {
-                case 0: v = block_value<0>(w, c); break;
-                case 1: v = block_value<1>(w, c); break;
-                case 2: v = block_value<2>(w, c); break;
-                default: v = block_value<3>(w, c); break;
-            }
             // (the fold of a unit's first block is of acc = 0: skipped when no
             // group of the wave is past its first block, e.g. one-block units)
-            if (__builtin_amdgcn_readfirstlane(__any(k != 0))) acc = apply_op<4>(kAuxSpanFold, acc);
-            acc ^= v;
+            const bool fold = __builtin_amdgcn_readfirstlane(__any(k != 0));
+            switch (nskip) {
+                case 0: acc = block_fold<0>(acc, fold, w, c); break;
+                case 1: acc = block_fold<1>(acc, fold, w, c); break;
+                case 2: acc = block_fold<2>(acc, fold, w, c); break;
+                default: acc = block_fold<3>(acc, fold, w, c); break;
+            }
         }
         if (last) {
             if (cur.valid()) {
@@ -1041,7 +1014,7 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
 // was one block and whose fragment the span's thread takes (none for len 0).
 __device__ __forceinline__ uint32_t span_units(const uint8_t *p, uint32_t len) {
     if (len == 0) return 0;
-    const uint32_t vlen = len + tail_pad(p, len);
+    const uint32_t vlen = len + grid_pad(p, len);
     const uint32_t ns = nseg_of(vlen);
     const SpanHead h = span_head(p, len);
     return ns - (h.drop && h.g1o == vlen - (uint64_t)(ns - 1) * kSegBytes ? 1u : 0u);
@@ -1051,7 +1024,7 @@ __device__ __forceinline__ uint32_t span_units(const uint8_t *p, uint32_t len) {
 // niters (make_unit) when it is one of them.
 __device__ __forceinline__ uint32_t span_blocks(const uint8_t *p, uint32_t len, uint32_t nu) {
     if (nu == 0) return 0;
-    const uint32_t vlen = len + tail_pad(p, len);
+    const uint32_t vlen = len + grid_pad(p, len);
     const uint32_t ns = nseg_of(vlen);
     constexpr uint32_t kSegBlocks = kSegBytes / kBlockBytes;
     if (nu < ns) return kSegBlocks * nu;
@@ -1084,7 +1057,7 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
         // (a whole span's R from the wave, whole_chunks: z = R ^ Z of its pieces)
         z = whole ? rwhole ^ span_corr_pieces(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow)
                   : span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow);
-        if (MODE == 1) z ^= t8.zeros(~it.aux, tail_pad(it.p, it.len));  // W
+        if (MODE == 1) z ^= mulmodp_dev(~it.aux, a.xpow[grid_pad(it.p, it.len)]);  // W
     }
     irec[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32) | (it.sane ? 0u : kInsane), it.len, z);
     a.span_acc[i] = 0u;
@@ -1166,7 +1139,7 @@ __global__ __launch_bounds__(kCountThreads) void k_count(SpanArgs a, uint64_t *n
         const bool valid = i < n;
         ItemDesc it{a.base, 0u, 0u, false};
         if (valid) it = fetch_item<MODE>(a, i);
-        const uint32_t t = tail_pad(it.p, it.len);
+        const uint32_t t = grid_pad(it.p, it.len);
         const uint64_t kh = (uintptr_t)it.p & 15u, off = (uint64_t)(it.p - a.base);
         const SpanHead h = span_head(it.p, it.len);
         const bool whole = valid && it.sane && it.len != 0 && h.drop && h.g1o == (uint64_t)it.len + t;
@@ -1310,7 +1283,7 @@ constexpr uint32_t kExpandInlineDn = 8;
 
 // First segment of span i that is a unit (1 when the head segment is not).
 __device__ __forceinline__ uint32_t first_seg(const uint8_t *p, uint32_t len, uint32_t nunit) {
-    return nunit ? nseg_of(len + tail_pad(p, len)) - nunit : 0u;
+    return nunit ? nseg_of(len + grid_pad(p, len)) - nunit : 0u;
 }
 
 // Balanced plan (starts != nullptr).  T = the blocks of all units, G = the
@@ -1498,7 +1471,7 @@ __global__ void k_final(SpanArgs a, const uint4 *irec) {
             p = a.base + (sane ? off : 0);
             len = a.len;
             const SpanHead h = span_head(p, len);
-            R = sane && !(h.drop && h.g1o == len + tail_pad(p, len)) ? a.out[i] : 0u;  // (else not given to k_spans)
+            R = sane && !(h.drop && h.g1o == len + grid_pad(p, len)) ? a.out[i] : 0u;  // (else not given to k_spans)
             if (sane) z = span_corr(p, len, a.crc_in ? a.crc_in[i] : 0u, t8, a.xpow);
         }
         if (MODE == 1) {
@@ -1506,7 +1479,7 @@ __global__ void k_final(SpanArgs a, const uint4 *irec) {
             a.ok[i] = good;
             nb += !good;
         } else {
-            const uint32_t t = tail_pad(p, len);
+            const uint32_t t = grid_pad(p, len);
             uint32_t v = R ^ z;
             if (t) v = mulmodp_dev(v, a.xpow[kXpowInv + t]);
             emit<MODE>(a, i, ~v, sane, p);
@@ -1564,8 +1537,8 @@ __global__ __launch_bounds__(1024) void k_small(SpanArgs a, const uint4 *__restr
         load_block(w, d, k, li, zero);
     };
     auto reduce = [&](const BlockWin &w, uint32_t k) {
-        const uint32_t v = block_value<0>(w, c);
-        if (k < niters) acc = apply_op<4>(kAuxSpanFold, acc) ^ v;
+        const uint32_t v = block_fold<0>(acc, true, w, c);
+        if (k < niters) acc = v;
     };
     BlockWin w0, w1;
     if (nmax) issue(w0, 0);
@@ -1643,7 +1616,7 @@ __global__ __launch_bounds__(1024) void k_small(SpanArgs a, const uint4 *__restr
 // block: vmcnt counts in issue order, so when the address is needed only the
 // newer block loads may still be pending.
 struct BlkRegs {
-    ItemRegs<32, 32, 4> d;
+    K1Regs d;       // the block, in K1's lane layout
     uint4 rec;      // descriptor of the block this buffer loads next
     uint32_t rs;    // (planned) its span
     uint32_t sidx;  // (planned) the span of the block two loads later
@@ -1697,7 +1670,7 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
         bool sane = !(r.y & kInsane);
         if (IDENT) sane = off <= a.base_bytes && r.z <= a.base_bytes - off;  // (as decode_unit)
         const uint8_t *e = a.base + off + r.z;
-        const uint8_t *blk = e + ((0u - (uint32_t)(uintptr_t)e) & 15u) - kBlockBytes;  // (pointer
+        const uint8_t *blk = e + ((0u - (uint32_t)(uintptr_t)e) & (kGridAlign - 1)) - kBlockBytes;  // (pointer
         return sane ? blk : zero;  // arithmetic: an integer round trip would make these flat loads)
     };
     // Loads run ahead of their use (vmcnt counts in issue order, so when a
@@ -1705,7 +1678,7 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
     // steps ahead, the descriptor two, the block one.
     auto ld = [&](BlkRegs &b, uint64_t gi) {
         if (IDENT && !OFFS) {  // (fixed stride: nothing to load ahead)
-            b.d.load(block_of(rec_of(j_of(gi), 0u)), li);
+            b.d.template load_at<kSpanNT>(block_of(rec_of(j_of(gi), 0u)), li * kK1LaneBytes);
         } else {
             const uint8_t *blk = block_of(b.rec);
             if (!IDENT) {
@@ -1714,13 +1687,13 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
             }
             b.rec = rec_of(j_of(gi + 2 * gstep), b.rs);
             if (!IDENT) b.sidx = fastidx[j_of(gi + 4 * gstep)];
-            b.d.load(blk, li);
+            b.d.template load_at<kSpanNT>(blk, li * kK1LaneBytes);
         }
         // (as K1: the loads stay at the top of the step instead of being sunk
         // into the chains, where the next step would wait on them at once)
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto part0 = [&](const BlkRegs &b) { return reduce_level<0>(lane_partial_x3s<32>(b.d, c), (lane & 1u) == 0u); };
+    auto part0 = [&](const BlkRegs &b) { return reduce_level<0>(k1_lane_value(b.d, c), (lane & 1u) == 0u); };
     uint32_t *dst = IDENT ? a.out : a.span_acc;
     auto store = [&](uint32_t raw, uint64_t gi, uint32_t span, bool on) {
         const uint64_t item = item_of(gi);
@@ -1750,7 +1723,7 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
         const uint32_t vc = part0(ra), sc = ra.cur;
         ld(ra, grp + 4 * gstep);
         const uint32_t vd = part0(rb), sd = rb.cur;
-        const uint32_t raw = group_reduce32_quad(vab, group_pair_level1(vc, vd, lane), lane);
+        const uint32_t raw = group_reduce32_quad_span(vab, group_pair_level1(vc, vd, lane), lane);
         const uint32_t sp = li == 0 ? sa : li == 1 ? sb : li == 2 ? sc : sd;
         store(raw, grp + (li & 3u) * gstep, sp, li < 4);
         grp += 4 * gstep;
@@ -1760,11 +1733,17 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
         const uint32_t va = part0(ra), sa = ra.cur;
         ld(ra, grp + 2 * gstep);
         const uint32_t vb = part0(rb), sb = rb.cur;
-        const uint32_t raw = group_reduce32_pair(va, vb, lane);
+        const uint32_t raw = group_reduce32_pair_span(va, vb, lane);
         store(raw, li == 0 ? grp : grp + gstep, li == 0 ? sa : sb, li < 2);
         grp += 2 * gstep;
     }
-    if (nsteps & 1) store(group_reduce32_dpp(lane_partial_x3s<32>(ra.d, c), lane), grp, ra.cur, li == 0);
+    if (nsteps & 1) {
+        uint32_t v = part0(ra);
+        v = reduce_level<1>(v, (lane & 3u) == 0u);
+        v = reduce_level<2>(v, (lane & 7u) == 0u);
+        v = reduce_level<3>(v, (lane & 15u) == 0u);
+        store(reduce_level4_span(v, (lane & 31u) == 0u), grp, ra.cur, li == 0);
+    }
 }
 
 // ===========================================================================

@@ -63,7 +63,6 @@ namespace {
 constexpr int kBlock = 1024;                    // 16 waves, 32 lane groups
 constexpr uint32_t kItemsPerBlockStep = 32;     // one span per 32-lane group
 constexpr uint32_t kFixedLen = mcrc_dev::kK1Bytes;  // K1: 8 pieces x 32 lanes x 16 B
-static_assert(mcrc_dev::kK1CH == mcrc_dev::kSpanCH, "k_small, k_blocks and the span kernels share the row layout");
 
 thread_local float g_last_kernel_ms = -1.0f;
 
@@ -77,10 +76,8 @@ struct Device {
     int id = -1;
     int cus = 0;
     bool ok = false;
-    uint4 *img = nullptr;       // LDS table image of the span kernels (crc32c_gf2.h build_lds_image_span)
+    uint4 *img = nullptr;       // LDS table image of every table kernel (build_lds_image_span, chunk 16)
     uint32_t *tab8 = nullptr;   // byte-wise table (k_count / k_final: a span's head fragment and foreign bytes)
-    uint4 *img_k1 = nullptr;    // row image (160 KiB, crc32c_gf2.h build_lds_image_k1): k_small, k_blocks
-    uint4 *img_k1c = nullptr;   // K1 image: build_lds_image_span at chunk 16 (K1's 16-B lane pieces)
     uint32_t *xpow = nullptr;   // x^(8n) table (layout mcrc_dev::kXpow*)
     uint32_t *xk = nullptr;     // k_lines: x^(8e), e in [kXkLo, kXkLo + kXkN)
     uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
@@ -221,8 +218,11 @@ int init_device(Device &d, int id) {
     HIP_OK(hipGetDeviceProperties(&p, id));
     if (strncmp(p.gcnArchName, "gfx950", 6) != 0) return CRC32C_ENODEV;
     d.cus = p.multiProcessorCount;
+    // the table image of every table kernel: slice-by-4 tables replicated per
+    // bank, the lane tree on 16-B granules, the half-item fold M_2048 and the
+    // shifted last steps (crc32c_gf2.h build_lds_image_span at chunk 16)
     std::vector<uint32_t> img(mcrc::kImageK1Dwords);
-    mcrc::build_lds_image_span(img.data(), mcrc_dev::kSpanCH);
+    mcrc::build_lds_image_span(img.data(), mcrc_dev::kK1LaneBytes);
     std::vector<uint32_t> tab8(mcrc_dev::kTab8Dwords);  // [k][b]: the byte-wise table followed by k zero bytes
     mcrc::build_t0(tab8.data());
     for (uint32_t k = 1; k < 16; ++k) {
@@ -238,19 +238,12 @@ int init_device(Device &d, int id) {
         xp[1024 + j] = mcrc::xpow8n((uint64_t)j << 10);
         xp[2048 + j] = mcrc::xpow8n((uint64_t)j << 20);
     }
-    for (uint32_t t = 0; t < mcrc_dev::kTailAlign; ++t) xp[mcrc_dev::kXpowInv + t] = mcrc::xpow8n_inv(t);
+    for (uint32_t t = 0; t < mcrc_dev::kGridAlign; ++t) xp[mcrc_dev::kXpowInv + t] = mcrc::xpow8n_inv(t);
     for (uint32_t j = 0; j < 8; ++j) xp[mcrc_dev::kXpowL3 + j] = mcrc::xpow8n((uint64_t)j << 30);
     HIP_OK(hipMalloc(&d.img, img.size() * 4));
     HIP_OK(hipMemcpy(d.img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&d.tab8, tab8.size() * 4));
     HIP_OK(hipMemcpy(d.tab8, tab8.data(), tab8.size() * 4, hipMemcpyHostToDevice));
-    std::vector<uint32_t> img_k1(mcrc::kImageK1Dwords);
-    mcrc::build_lds_image_k1(img_k1.data(), mcrc_dev::kK1CH);
-    HIP_OK(hipMalloc(&d.img_k1, img_k1.size() * 4));
-    HIP_OK(hipMemcpy(d.img_k1, img_k1.data(), img_k1.size() * 4, hipMemcpyHostToDevice));
-    mcrc::build_lds_image_span(img_k1.data(), mcrc_dev::kK1LaneBytes);
-    HIP_OK(hipMalloc(&d.img_k1c, img_k1.size() * 4));
-    HIP_OK(hipMemcpy(d.img_k1c, img_k1.data(), img_k1.size() * 4, hipMemcpyHostToDevice));
     // rows k (k < kSegpowLo) and kSegpowLo + j (x^(8 * 4096 * kSegpowLo j))
     // for every block shift in a 4 GiB span (a unit's shift: the blocks from
     // its end to the span's end)
@@ -400,10 +393,12 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
 }
 
 // Every span of `len` bytes is one whole block at its G1 (mcrc_dev::one_block)
-// whatever its alignment (p & 15): the identity batch can go to k_blocks.
+// whatever its alignment (p mod 128, the grid's line): the identity batch can
+// go to k_blocks.
 bool one_block_len(uint32_t len) {
-    for (uint32_t kh = 0; kh < 16; ++kh) {
-        const uint32_t vlen = len + ((0u - kh - len) & (mcrc_dev::kTailAlign - 1)), x = vlen + kh;
+    for (uint32_t al = 0; al < mcrc_dev::kGridAlign; ++al) {
+        const uint32_t kh = al & 15u;
+        const uint32_t vlen = len + ((0u - al - len) & (mcrc_dev::kGridAlign - 1)), x = vlen + kh;
         const uint32_t g1o = x - mcrc_dev::kBlockBytes * ((x - 1) / mcrc_dev::kBlockBytes) - kh;
         const bool drop = len && (g1o <= mcrc_dev::kFragMax || vlen <= mcrc_dev::kWholeMax);  // frag_drop
         if (!(drop ? vlen - g1o == mcrc_dev::kBlockBytes : len && x == mcrc_dev::kBlockBytes)) return false;
@@ -432,7 +427,7 @@ void launch_k5(const Device &d, const mcrc_dev::SpanArgs &a, mcrc_dev::ItemsOut 
     io.xk = d.xk;
     io.nsr = (uint32_t)std::min<uint64_t>(mcrc_dev::kEpoch, std::max<uint64_t>(1, (a.n + 2 * waves - 1) / (2 * waves)));
     hipLaunchKernelGGL((mcrc_dev::k_lines<MODE, OFFS>), dim3(grid), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st, a,
-                       d.img_k1c, io);
+                       d.img, io);
 }
 
 // Large item batches go through launch_items, where k_census samples their
@@ -524,14 +519,14 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     }
     if (identity) {
         // (spans of at most kWholeMax - 15 bytes are all their threads' in k_final)
-        if (a.len + mcrc_dev::kTailAlign - 1 > mcrc_dev::kWholeMax) {
+        if (a.len + mcrc_dev::kGridAlign - 1 > mcrc_dev::kWholeMax) {
             if (one_block_len(a.len) && a.offsets)
                 hipLaunchKernelGGL((mcrc_dev::k_blocks<true, true>), dim3(grid_for(d, n)), dim3(1024),
-                                   mcrc_dev::kLdsImageK1Bytes, st, a, d.img_k1, (const uint4 *)nullptr,
+                                   mcrc_dev::kLdsImageK1Bytes, st, a, d.img, (const uint4 *)nullptr,
                                    (const uint32_t *)nullptr, (const uint32_t *)nullptr);
             else if (one_block_len(a.len))
                 hipLaunchKernelGGL((mcrc_dev::k_blocks<true, false>), dim3(grid_for(d, n)), dim3(1024),
-                                   mcrc_dev::kLdsImageK1Bytes, st, a, d.img_k1, (const uint4 *)nullptr,
+                                   mcrc_dev::kLdsImageK1Bytes, st, a, d.img, (const uint4 *)nullptr,
                                    (const uint32_t *)nullptr, (const uint32_t *)nullptr);
             else
                 spans(a, grid_for(d, n));
@@ -578,7 +573,7 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     // spans whose unit is one whole block: k_blocks over the compacted list;
     // the other spans' units: the span kernel
     hipLaunchKernelGGL((mcrc_dev::k_blocks<false, true>), dim3(grid_for(d, n)), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st,
-                       u, d.img_k1, (const uint4 *)d.irec, (const uint32_t *)d.fastidx, (const uint32_t *)nfast);
+                       u, d.img, (const uint4 *)d.irec, (const uint32_t *)d.fastidx, (const uint32_t *)nfast);
     spans(u, d.cus);
     mcrc_dev::SpanArgs w = u;  // (every table pointer set, even those whole units do not use)
     w.units = d.whole;
@@ -678,10 +673,10 @@ bool k1_shape(const crc32c_spans &s) {
 int launch_k1(const Device &d, const crc32c_spans &s, hipStream_t st) {
     if (s.crc_in)
         hipLaunchKernelGGL((mcrc_dev::k_fixed<true>), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
-                           st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1c, s.crc_in, s.out);
+                           st, (const uint8_t *)s.base, s.stride, s.n, d.img, s.crc_in, s.out);
     else
         hipLaunchKernelGGL((mcrc_dev::k_fixed<false>), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
-                           st, (const uint8_t *)s.base, s.stride, s.n, d.img_k1c, s.crc_in, s.out);
+                           st, (const uint8_t *)s.base, s.stride, s.n, d.img, s.crc_in, s.out);
     HIP_OK(hipGetLastError());
     return CRC32C_OK;
 }

@@ -12,9 +12,13 @@ POLY = 0x82F63B78
 M32 = 0xFFFFFFFF
 
 
+GRID = 128  # kGridAlign: the planned path's grid is anchored at E rounded up to a 128-B line
+
+
 def tail_pad(p, length):
-    """t = Ea - E, Ea = E rounded up to 16."""
-    return (-(p + length)) & 15
+    """t = Ea - E, Ea = E rounded up to a 128-B line (grid_pad; round 5,
+    it was 16 before)."""
+    return (-(p + length)) & (GRID - 1)
 
 
 def nseg_of(vlen):
@@ -73,18 +77,16 @@ def units_of(base, off, length):
 
 
 def real_pieces(p, eo, niters, k):
-    """Addresses of the pieces load_block reads from memory for block k."""
+    """Addresses of the pieces load_block reads from memory for block k (K1's
+    lane layout: lane li's piece j at G + 512 j + 16 li)."""
     grel = eo - BLOCK * (niters - k)
     out = []
     for li in range(32):
-        lrel = grel + 32 * li
+        lrel = grel + 16 * li
         e0 = lrel + 16 + (p & 15) if niters else -BLOCK - 16
-        for r in range(4):
-            er = e0 + 1024 * r
-            if er > 0:
-                out.append(p + lrel + 1024 * r)
-            if er + 16 > 0:
-                out.append(p + lrel + 1024 * r + 16)
+        for j in range(8):
+            if e0 + 512 * j > 0:
+                out.append(p + lrel + 512 * j)
     return out
 
 

@@ -46,6 +46,55 @@ using namespace mcrc_dev;
 
 constexpr uint64_t kItems = 1ull << 20, kItemBytes = 4096;
 
+// Round 4's K1 pieces, removed from the product in round 5 and kept here for
+// k1load / k1nt: a lane's 32 contiguous bytes of each 1 KiB row, four row
+// chains, the tree on 32-B granules (the row image build_lds_image_k1 at
+// chunk 32, level 4 at tables 16..19).
+constexpr uint32_t kK1Rows = 4, kK1CH = 32;
+template <int LPI, int CH, int R>
+struct ItemRegs {
+    static constexpr int Q = CH / 16;
+    uint4 d[R][Q];
+    uint32_t cin;
+};
+template <int CH>
+__device__ __forceinline__ uint32_t lane_partial_x3s(const ItemRegs<32, CH, 4> &it, const LaneCtx &c) {
+    constexpr int N = 4 * (CH / 16);
+    constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};
+    uint32_t x[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = it.d[r][0].x;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            x[r] = i + 1 < N ? step4_next(x[r], dw4(it.d[r][(i + 1) >> 2], (i + 1) & 3), c)
+                             : (r < 3 ? step4_last_shifted(x[r], kShift[r]) : step4_next(x[r], 0u, c));
+    return xor3(x[0], x[1], x[2]) ^ x[3];
+}
+__device__ __forceinline__ uint32_t group_reduce32_quad(uint32_t ab, uint32_t cd, uint32_t lane) {
+    const uint32_t cs = __builtin_amdgcn_update_dpp(0u, cd, 0x112, 0xf, 0xf, false);  // row_shr:2
+    uint32_t v = (lane & 2u) ? cs : ab;
+    v = reduce_level<2>(v, (lane & 7u) < 4u);
+    v = reduce_level<3>(v, (lane & 15u) < 4u);
+    return reduce_level<4>(v, (lane & 31u) < 4u);
+}
+__device__ __forceinline__ uint32_t group_reduce32_pair(uint32_t a, uint32_t b, uint32_t lane) {
+    const uint32_t bs = __builtin_amdgcn_update_dpp(0u, b, 0x111, 0xf, 0xf, false);  // row_shr:1
+    uint32_t v = (lane & 1u) ? bs : a;
+    v = reduce_level<1>(v, (lane & 3u) < 2u);
+    v = reduce_level<2>(v, (lane & 7u) < 2u);
+    v = reduce_level<3>(v, (lane & 15u) < 2u);
+    return reduce_level<4>(v, (lane & 31u) < 2u);
+}
+__device__ __forceinline__ uint32_t group_reduce32_dpp(uint32_t v, uint32_t lane) {
+    v = reduce_level<0>(v, (lane & 1u) == 0u);
+    v = reduce_level<1>(v, (lane & 3u) == 0u);
+    v = reduce_level<2>(v, (lane & 7u) == 0u);
+    v = reduce_level<3>(v, (lane & 15u) == 0u);
+    return reduce_level<4>(v, (lane & 31u) == 0u);
+}
+
 // K1's wave -> contiguous range of item pairs (crc32c_kernels.hip k_fixed)
 struct Range {
     uint64_t g0, g1;
