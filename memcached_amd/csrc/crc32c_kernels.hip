@@ -227,16 +227,20 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 //
 // Pieces as they lie.  A span D = [p, E) is read as the 16-B aligned pieces
 // [ph, Ea), ph = p rounded down to 16 and Ea = E rounded up to a 128-B line
-// (grid_pad, round 5; 16 before),
-// foreign bytes included: the span kernel computes R = raw([ph, Ea)) with no
-// masking and no initial value.  With F_h = [ph, p), F_t = [E, Ea),
-// t = |F_t|, the algebra of crc32c.c:58-137 gives
-//   raw([ph, Ea)) = M_{|D|+t}(raw(F_h)) ^ M_t(raw(D)) ^ raw(F_t), so
-//   crc32c(c, D) = ~M_{-t}(R ^ Z),   Z = M_{|D|+t}(~c ^ raw(F_h)) ^ raw(F_t).
-// Z depends only on c and the at most 30 foreign bytes, so one thread per
-// span computes it (span_corr: k_count before the span kernel, or k_final
-// after it), at a thirty-second of the cost of doing it in a 32-lane group;
-// the span kernel's per-unit work is its lane reduction and one store.
+// (grid_pad, round 5; 16 before), the head's foreign bytes F_h = [ph, p)
+// included and the tail's F_t = [E, Ea) cleared in registers (the last line
+// of the span's last block, mask_tail; round 5): the span kernel computes
+// R = raw([ph, E) followed by t = |F_t| zeros) with no initial value.  The
+// algebra of crc32c.c:58-137 gives
+//   R = M_{|D|+t}(raw(F_h)) ^ M_t(raw(D)), so
+//   crc32c(c, D) = ~M_{-t}(R ^ Z),   Z = M_{|D|+t}(~c ^ raw(F_h)).
+// Z depends only on c and the at most 15 bytes of F_h, which share the head
+// piece (and for item images the header's line), so one thread per span
+// computes it (span_corr: k_count before the span kernel, or k_final after
+// it), at a thirty-second of the cost of doing it in a 32-lane group; the
+// span kernel's per-unit work is its lane reduction and one store.  (Until
+// round 5 the thread also read F_t and XORed raw(F_t) into Z: a line per
+// span that the span kernel reads again.)
 //
 // Work units.  A virtual span longer than kSegBytes is cut into segments of
 // kSegBytes anchored at Ea (segment 0, the head, holds the remainder: 17 B to
@@ -525,14 +529,14 @@ __device__ __forceinline__ bool one_block(const uint8_t *p, uint32_t len, const 
 }
 
 // Z of span [p, p + len) with initial CRC c (see "Pieces as they lie"), for
-// the R that the span kernel computes over the span's units:
+// the R that the span kernel computes over the span's units (F_t cleared):
 // - no bytes: the kernel reads nothing (R = 0), Z = M_t(~c);
 // - head fragment taken (span_head): the kernel reads [G1, Ea), so
-//   Z = M_{Ea-G1}(r) ^ raw(F_t) with r = the register from ~c over [p, G1),
+//   Z = M_{Ea-G1}(r) with r = the register from ~c over [p, G1),
 //   or, when G1 = Ea, Z = M_t(register from ~c over D);
-// - otherwise Z = M_{len+t}(~c ^ raw(F_h)) ^ raw(F_t): raw(F_h) = raw of the
-//   head piece's first kh bytes moved to its top (leading zeros leave a zero
-//   register unchanged), raw(F_t) = raw of the t bytes after E.
+// - otherwise Z = M_{len+t}(~c ^ raw(F_h)): raw(F_h) = raw of the head
+//   piece's first kh bytes moved to its top (leading zeros leave a zero
+//   register unchanged).
 // One thread.
 // Z when the kernel's R covers the pieces [ph, Ea) as they lie (the third
 // case above; also k_count's wave-cooperative whole spans, whole_chunks).
@@ -542,9 +546,7 @@ __device__ __forceinline__ uint32_t span_corr_pieces(const uint8_t *p, uint32_t 
     const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
     uint32_t y = ~c;
     if (kh) y ^= raw16(shl_bytes(ld_piece(p - kh), 16 - kh), t8);  // raw(F_h)
-    uint32_t z = mulmodp_dev(y, xpow8_dev(xp, (uint64_t)len + t));
-    if (t) z ^= reg_advance(0u, p + len, t, t8);  // raw(F_t)
-    return z;
+    return mulmodp_dev(y, xpow8_dev(xp, (uint64_t)len + t));
 }
 __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
                                               const uint32_t *xp) {
@@ -556,9 +558,7 @@ __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, ui
     if (!h.drop) return span_corr_pieces(p, len, c, t8, xp);
     // Ea - G1 is whole blocks; one block (every one-block span) is a table step
     const uint32_t r = reg_advance(~c, p, (uint32_t)h.g1o, t8);
-    uint32_t z = vlen - h.g1o == kBlockBytes ? t8.block(r) : mulmodp_dev(r, xpow8_dev(xp, vlen - h.g1o));
-    if (t) z ^= reg_advance(0u, p + len, t, t8);  // raw(F_t)
-    return z;
+    return vlen - h.g1o == kBlockBytes ? t8.block(r) : mulmodp_dev(r, xpow8_dev(xp, vlen - h.g1o));
 }
 
 
@@ -646,11 +646,14 @@ constexpr uint32_t kInsane = 0x80000000u;
 struct UnitDesc {
     const uint8_t *p;  // first byte of this unit
     uint32_t eo;       // e - p: e = 16-aligned end of this unit's grid
-    uint32_t nf;       // niters << 8 | flags
+    uint32_t nf;       // niters << 12 | tail << 4 | flags (tail: bytes of F_t before e, the
+                       // span's grid end, when this unit ends there; else 0)
     uint32_t raw;      // this lane's dword li & 7 of the unit's raw record: span index (dword 5)
                        // and segment (dword 7) are gathered from it when the unit ends
     static constexpr uint32_t kValid = 1, kSingle = 2, kHead = 4, kSane = 8;
-    __device__ __forceinline__ uint32_t niters() const { return nf >> 8; }
+    static constexpr uint32_t kNitersShift = 12, kTailShift = 4;
+    __device__ __forceinline__ uint32_t niters() const { return nf >> kNitersShift; }
+    __device__ __forceinline__ uint32_t tail() const { return (nf >> kTailShift) & 127u; }
     __device__ __forceinline__ bool valid() const { return nf & kValid; }
     __device__ __forceinline__ bool single() const { return nf & kSingle; }
     __device__ __forceinline__ bool head() const { return nf & kHead; }
@@ -727,7 +730,11 @@ __device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw,
     if (UNITS) {
         d.p = a.base + ((uint64_t)__shfl(raw, g | 0, 64) | ((uint64_t)__shfl(raw, g | 1, 64) << 32));
         d.eo = __shfl(raw, g | 2, 64);
-        d.nf = __shfl(raw, g | 6, 64);
+        // (record dword 6: niters << 8 | flags; dword 3: E - p, past e for
+        // every unit but the span's last, whose tail is e - E = t < 128)
+        const uint32_t ew = __shfl(raw, g | 3, 64), r6 = __shfl(raw, g | 6, 64);
+        const uint32_t tl = d.eo > ew ? d.eo - ew : 0u;
+        d.nf = (r6 & 15u) | (tl << UnitDesc::kTailShift) | ((r6 >> 8) << UnitDesc::kNitersShift);
     } else {
         // unit = span u of `len` bytes at `off`: make_unit(kWhole) restated in
         // 32-bit arithmetic (everything but the address depends on p & 15 only;
@@ -746,7 +753,9 @@ __device__ __forceinline__ UnitDesc decode_unit(const SpanArgs &a, uint32_t raw,
         const uint32_t niters = len ? (eo + ((kh + po) & 15u) + kBlockBytes - 1) >> 12 : 0u;
         d.p = a.base + (sane ? off : 0) + po;
         d.eo = eo;
-        d.nf = u < nunits ? UnitDesc::kValid | UnitDesc::kSingle | (niters << 8) : 0u;  // flags 0: no unit
+        d.nf = u < nunits ? UnitDesc::kValid | UnitDesc::kSingle | ((vlen - len) << UnitDesc::kTailShift) |
+                                (niters << UnitDesc::kNitersShift)
+                          : 0u;  // flags 0: no unit
     }
     return d;
 }
@@ -782,6 +791,22 @@ __device__ __forceinline__ void load_block(BlockWin &w, const UnitDesc &d, uint3
         const uint8_t *q = e0 + j * (int32_t)kK1Piece > 0 ? q0 + j * kK1Piece : zl;
         w.v[j] = kSpanNT ? ld16_nt(q) : ld16(q);
     }
+}
+
+// F_t cleared: the span's grid ends at Ea = E + t (t < 128), so F_t lies in
+// the last line of its last block, piece 7 of lanes 24..31 (lane li's piece
+// 7 is the line's bytes [16 (li - 24), +16)); the bytes of that piece from E
+// on, min(max(t - 16 (31 - li), 0), 16) of them, are cleared.
+__device__ __forceinline__ uint4 mask_tail(uint4 v, uint32_t t, uint32_t li) {
+    const int32_t cl = min(max((int32_t)t - 16 * (31 - (int32_t)li), 0), 16);  // bytes cleared
+    const int32_t keep = 16 - cl;
+    uint32_t m[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int32_t kb = min(max(keep - 4 * i, 0), 4);
+        m[i] = kb >= 4 ? ~0u : (1u << (8 * kb)) - 1u;
+    }
+    return make_uint4(v.x & m[0], v.y & m[1], v.z & m[2], v.w & m[3]);
 }
 
 // acc' = M_4096(acc) ^ (the block's lane value) = M_2048(M_2048(acc) ^ u_A) ^ u_B
@@ -948,6 +973,7 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         for (int j = 0; j < (int)kK1Pieces; ++j)
             asm volatile("" ::"v"(w.v[j].x), "v"(w.v[j].y), "v"(w.v[j].z), "v"(w.v[j].w));
         if (cur.niters()) {
+            if (__any(last && cur.tail())) w.v[kK1Pieces - 1] = mask_tail(w.v[kK1Pieces - 1], last ? cur.tail() : 0u, li);
             const int32_t grel = (int32_t)cur.eo - (int32_t)(kBlockBytes * (cur.niters() - k));  // G - p
             // rows wholly before p for every lane of the wave are skipped
             // (a group without a unit has niters == 0 and votes to skip)
@@ -1037,8 +1063,9 @@ __device__ __forceinline__ uint32_t span_blocks(const uint8_t *p, uint32_t len, 
 // Units and blocks per span (packed, units | blocks << 32: one exclusive scan
 // places the work units and the balanced plan's group boundaries), and
 // the span's item record with its z (the header is parsed once per launch, and
-// the foreign bytes of the head and tail pieces are read here: for packed
-// images they share lines with the headers this pass reads anyway).
+// the foreign bytes of the head piece are read here: for packed images they
+// share a line with the header this pass reads anyway; the tail's are
+// cleared by the span kernel and not read, round 5).
 // Span i's plan entries: one-block flag, unit count, item record, R = 0.
 template <int MODE>
 __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const ItemDesc &it, const Tab8 &t8,
@@ -1063,22 +1090,26 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
     a.span_acc[i] = 0u;
 }
 
-// R = raw of [ph, Ea) (the pieces as they lie) for every lane of the wave
-// whose span is whole (span_corr's first case: the thread's alone).  A whole
+// R = raw of [ph, Ea) (the pieces as they lie, F_t = [E, Ea) cleared as the
+// span kernel clears it) for every lane of the wave whose span is whole
+// (span_corr's first case: the thread's alone).  A whole
 // span's chain used to run in its lane while the lanes without one idled
 // (one whole span in seven on the mixed pages: 0.11 of k_count's 0.21 ms);
 // now the wave cuts the pieces of all its whole spans into 128-B chunks and
 // every lane takes one: r_c = raw of its <= 8 pieces, shifted past the rest of
 // its span (M_{Ea - end}, x^(8 n) from the xpow table), XORed into the span's
-// slot (LDS, wave-private).  tests/test_count_whole_model.py restates it.
+// slot (LDS, wave-private).  The chunks cover the pieces [ph, ceil16(E)) only
+// (the rest of [ph, Ea) is zeros), the piece holding E cleared from E on.
+// tests/test_count_whole_model.py restates it.
 constexpr uint32_t kCountThreads = 256;
 // (128-B chunks: half the x^(8n) multiplies of 64-B ones, mixed pages -0.6 %;
 // 256-B chunks' longer lane chains were slower: k_count_chunk_size_ab.txt)
 constexpr uint32_t kWholePieces = 8, kWholeChunk = 16 * kWholePieces;  // pieces / bytes per chunk
-__device__ __forceinline__ uint32_t whole_chunks(gbyte *gb, bool whole, uint64_t ph, uint64_t ea, const Tab8 &t,
-                                                 const uint32_t *xp, uint32_t *slot) {
+__device__ __forceinline__ uint32_t whole_chunks(gbyte *gb, bool whole, uint64_t ph, uint64_t e, uint64_t ea,
+                                                 const Tab8 &t, const uint32_t *xp, uint32_t *slot) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nch = whole ? (uint32_t)((ea - ph + kWholeChunk - 1u) / kWholeChunk) : 0u;
+    const uint64_t e16 = (e + 15u) & ~(uint64_t)15u;  // end of the pieces holding bytes of D
+    const uint32_t nch = whole ? (uint32_t)((e16 - ph + kWholeChunk - 1u) / kWholeChunk) : 0u;
     uint32_t inc = nch;  // inclusive chunk count over the wave
 #pragma unroll
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -1099,12 +1130,24 @@ __device__ __forceinline__ uint32_t whole_chunks(gbyte *gb, bool whole, uint64_t
                              ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ph >> 32), (int)s, 64) << 32);
         const uint64_t sea = (uint32_t)__shfl((int)(uint32_t)ea, (int)s, 64) |
                              ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ea >> 32), (int)s, 64) << 32);
+        const uint64_t se = (uint32_t)__shfl((int)(uint32_t)e, (int)s, 64) |
+                            ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(e >> 32), (int)s, 64) << 32);
+        const uint64_t se16 = (se + 15u) & ~(uint64_t)15u;
         const bool act = q < total;
         const uint64_t c0 = sph + (uint64_t)kWholeChunk * c;
-        const uint32_t np = act ? (uint32_t)min((sea - c0) >> 4, (uint64_t)kWholePieces) : 0u;
+        const uint32_t np = act ? (uint32_t)min((se16 - c0) >> 4, (uint64_t)kWholePieces) : 0u;
         Piece pc[kWholePieces];
 #pragma unroll
         for (uint32_t k = 0; k < kWholePieces; ++k) pc[k] = k < np ? ld_piece(gb + c0 + 16u * k) : Piece{0, 0};
+        // the last piece of the span: bytes from E on cleared (its first 16 - cl kept)
+        if (np && c0 + 16u * np == se16) {
+            const uint32_t keep = 16u - (uint32_t)(se16 - se);
+            const uint64_t mlo = keep >= 8 ? ~0ull : (1ull << (8 * keep)) - 1ull;
+            const uint64_t mhi = keep <= 8 ? 0ull : keep >= 16 ? ~0ull : (1ull << (8 * (keep - 8))) - 1ull;
+#pragma unroll
+            for (uint32_t k = 0; k < kWholePieces; ++k)
+                if (k + 1 == np) pc[k] = Piece{pc[k].lo & mlo, pc[k].hi & mhi};
+        }
         uint32_t r = 0;
 #pragma unroll
         for (uint32_t k = 0; k < kWholePieces; ++k) {
@@ -1143,7 +1186,7 @@ __global__ __launch_bounds__(kCountThreads) void k_count(SpanArgs a, uint64_t *n
         const uint64_t kh = (uintptr_t)it.p & 15u, off = (uint64_t)(it.p - a.base);
         const SpanHead h = span_head(it.p, it.len);
         const bool whole = valid && it.sane && it.len != 0 && h.drop && h.g1o == (uint64_t)it.len + t;
-        const uint32_t r = whole_chunks(gb, whole, off - kh, off + it.len + t, t8, a.xpow, slot);
+        const uint32_t r = whole_chunks(gb, whole, off - kh, off + it.len, off + it.len + t, t8, a.xpow, slot);
         if (valid) count_item<MODE>(a, i, it, t8, nunit, irec, fast, whole, r);
     }
 }
@@ -1532,7 +1575,8 @@ __global__ __launch_bounds__(1024) void k_small(SpanArgs a, const uint4 *__restr
         UnitDesc d;
         d.p = it.p;
         d.eo = eo;
-        d.nf = k < niters ? (niters << 8) | UnitDesc::kValid : 0u;  // (past the span: zeros)
+        // (past the span: zeros; no tail mask: k_small's grid is 16-B, its Z has raw(F_t))
+        d.nf = k < niters ? (niters << UnitDesc::kNitersShift) | UnitDesc::kValid : 0u;
         d.raw = 0;
         load_block(w, d, k, li, zero);
     };
@@ -1621,6 +1665,7 @@ struct BlkRegs {
     uint32_t rs;    // (planned) its span
     uint32_t sidx;  // (planned) the span of the block two loads later
     uint32_t cur;   // (planned) the span of the block in d
+    uint32_t tl;    // the block's span ends tl bytes before the block's end (F_t, mask_tail)
 };
 
 template <bool IDENT, bool OFFS>
@@ -1673,14 +1718,21 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
         const uint8_t *blk = e + ((0u - (uint32_t)(uintptr_t)e) & (kGridAlign - 1)) - kBlockBytes;  // (pointer
         return sane ? blk : zero;  // arithmetic: an integer round trip would make these flat loads)
     };
+    // t = Ea - E of the block's span (its F_t is the block's last t bytes)
+    auto tail_of = [&](const uint4 &r) -> uint32_t {
+        return (0u - ((uint32_t)(uintptr_t)a.base + r.x + r.z)) & (kGridAlign - 1);
+    };
     // Loads run ahead of their use (vmcnt counts in issue order, so when a
     // value is needed only newer loads may be pending): the span index four
     // steps ahead, the descriptor two, the block one.
     auto ld = [&](BlkRegs &b, uint64_t gi) {
         if (IDENT && !OFFS) {  // (fixed stride: nothing to load ahead)
-            b.d.template load_at<kSpanNT>(block_of(rec_of(j_of(gi), 0u)), li * kK1LaneBytes);
+            const uint4 r = rec_of(j_of(gi), 0u);
+            b.tl = tail_of(r);
+            b.d.template load_at<kSpanNT>(block_of(r), li * kK1LaneBytes);
         } else {
             const uint8_t *blk = block_of(b.rec);
+            b.tl = tail_of(b.rec);
             if (!IDENT) {
                 b.cur = b.rs;
                 b.rs = b.sidx;
@@ -1693,7 +1745,10 @@ __global__ __launch_bounds__(1024) void k_blocks(SpanArgs a, const uint4 *__rest
         // into the chains, where the next step would wait on them at once)
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto part0 = [&](const BlkRegs &b) { return reduce_level<0>(k1_lane_value(b.d, c), (lane & 1u) == 0u); };
+    auto part0 = [&](BlkRegs &b) {
+        b.d.d[kK1Pieces - 1] = mask_tail(b.d.d[kK1Pieces - 1], b.tl, li);
+        return reduce_level<0>(k1_lane_value(b.d, c), (lane & 1u) == 0u);
+    };
     uint32_t *dst = IDENT ? a.out : a.span_acc;
     auto store = [&](uint32_t raw, uint64_t gi, uint32_t span, bool on) {
         const uint64_t item = item_of(gi);

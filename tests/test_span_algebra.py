@@ -1,7 +1,8 @@
 """CPU check of the span kernels' algebra (crc32c_kernels.hip "Pieces as they
-lie", span_corr, k_final): with R = the XOR over a span's work units of
-M_{Ea - e}(raw of the unit's 16-B pieces as they lie in memory) -- what
-k_spans accumulates -- and Z from the span's thread,
+lie", span_corr, mask_tail, k_final): with R = the XOR over a span's work
+units of M_{Ea - e}(raw of the unit's 16-B pieces as they lie in memory, the
+span's tail bytes [E, Ea) cleared) -- what k_spans accumulates -- and Z from
+the span's thread,
     crc32c(c, D) = ~M_{-t}(R ^ Z)   and, for a verify,  R == W
 for every alignment, length class (empty, short, one block, head fragment
 taken or not, multi-segment) and initial CRC.  The expected CRC comes from the
@@ -33,12 +34,16 @@ def raw(data):
 
 def kernel_R(buf, p, length):
     """What k_spans accumulates for span [p, p + length) of buf."""
-    Ea = p + length + tail_pad(p, length)
+    E = p + length
+    Ea = E + tail_pad(p, length)
     R = 0
     for up, eo, niters, _single, _segk in units_of(0, p, length):
         e = up + eo
         lo = up - (up & 15) if niters else e  # load_block: pieces from floor16(p)
-        R ^= mulmodp(raw(buf[lo:e]), xpow8(Ea - e))
+        piece = bytearray(buf[lo:e])
+        if e > E:  # mask_tail: the last line's bytes from E on
+            piece[E - lo:] = bytes(e - E)
+        R ^= mulmodp(raw(piece), xpow8(Ea - e))
     return R
 
 
@@ -56,9 +61,6 @@ def span_corr(buf, p, length, c):
     else:
         kh = p & 15
         z = mulmodp(~c & M32 ^ raw(buf[p - kh:p]), xpow8(vlen))
-    if t:
-        E = p + length
-        z ^= raw(buf[E:E + t])
     return z
 
 
