@@ -1337,6 +1337,7 @@ __device__ __forceinline__ uint32_t first_seg(const uint8_t *p, uint32_t len, ui
 // starts[g] = j_g + g (j_g: the unit holding block g * per).  A boundary at a
 // unit's first block leaves an empty record, the end of group g - 1's list.
 // Round robin (starts == nullptr): unit j is record j.
+constexpr uint32_t kBalanceMinPer = 2;
 struct Balance {
     uint32_t *starts;
     uint64_t per;  // blocks per group
@@ -1347,12 +1348,15 @@ struct Balance {
 __device__ __forceinline__ Balance balance_of(const PlanSum *total, uint64_t n, uint32_t groups, uint32_t *starts) {
     Balance b{starts, 1, 0};
     if (starts && n) {
-        // (at least a segment's blocks per group: a small batch -- e.g. K5's
-        // fallback list of a few long images -- would otherwise cut every
-        // unit into one record per block, serially in its span's thread of
-        // k_expand, ~0.3 ms for 50 images of 1-2 MiB)
+        // (at least kBalanceMinPer blocks per group.  One per block cut every
+        // unit of a small batch into one record per block, serially in its
+        // span's thread of k_expand: ~0.3 ms for 50 images of 1-2 MiB before
+        // k_expand_big took the long spans of a device-counted list
+        // (kExpandInlineDn).  A segment's 16, the floor until round 5, left a
+        // small batch on few groups: K5's fallback list of ~1400 blocks per
+        // 300 pages ran as 88 groups of 16 serial blocks, k_spans 0.07 ms.)
         const uint64_t t = total->blocks;
-        b.per = max((t + groups - 1) / groups, (uint64_t)(kSegBytes / kBlockBytes));
+        b.per = max((t + groups - 1) / groups, (uint64_t)kBalanceMinPer);
         b.gm = (t + b.per - 1) / b.per;
     }
     return b;

@@ -154,6 +154,7 @@ def one_block(p, length):
 # --- balanced plan (crc32c_kernels.hip span_blocks, unit_piece, put_unit) ---
 
 SEG_BLOCKS = SEG // BLOCK
+BALANCE_MIN_PER = 2  # kBalanceMinPer
 
 
 def span_blocks(p, length):
@@ -194,7 +195,7 @@ def balanced_plan(spans, groups):
         for up, eo, nb, single, segk in units_of(0, p, length):
             units.append((s, (up, eo, nb, single, SEG_BLOCKS * segk)))
     t = sum(u[2] for _, u in units)
-    per = max(-(-t // groups), SEG_BLOCKS)  # (k_expand: at least a segment's blocks per group)
+    per = max(-(-t // groups), BALANCE_MIN_PER)  # (k_expand: at least kBalanceMinPer blocks per group)
     gm = -(-t // per)
     starts = {0: 0}
     records = []

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from tests import oracle
-from tests.span_model import (BLOCK, M32, SEG, balanced_plan, mulmodp, span_blocks, span_units, tail_pad,
+from tests.span_model import (BALANCE_MIN_PER, BLOCK, M32, SEG, balanced_plan, mulmodp, span_blocks, span_units, tail_pad,
                               units_of, xpow8)
 
 
@@ -57,7 +57,7 @@ def test_groups_get_equal_contiguous_block_ranges(groups):
     want = [(s, b) for s, (p, length) in enumerate(spans) for u in units_of(0, p, length)
             for b in blocks_of((u[0], u[1], u[2], u[3], 0))]
     t = len(want)
-    assert per == max(-(-t // groups), SEG // BLOCK)  # (a segment's blocks at least)
+    assert per == max(-(-t // groups), BALANCE_MIN_PER)  # (kBalanceMinPer blocks at least)
     got = []
     for g in range(groups):
         if g * per >= t:
