@@ -112,6 +112,28 @@ __device__ __forceinline__ uint32_t k1_lane_value(const K1Regs &r, const LaneCtx
     return apply_op<4>(kAuxSpanFold, ua) ^ ub;
 }
 
+// Half an item's pieces for one lane (pieces 4 q .. 4 q + 3 of half q).
+struct K1Half {
+    uint4 d[4];
+    uint32_t cin;  // (half 0) the item's initial CRC
+};
+// The value of half Q: its four chains, each ended by its shifted last step
+// (M_1536, M_1024, M_512, plain: the half's pieces stand 512 (3 - k) from its
+// end); the item's lane value is M_2048(u_0) ^ u_1 (k1_lane_value).
+__device__ __forceinline__ uint32_t k1_half_value(const K1Half &r, const LaneCtx &c) {
+    constexpr uint32_t kShift[3] = {kAuxShift0, kAuxShift1, kAuxShift2};
+    uint32_t x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = r.d[k].x;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = step4_next(x[k], dw4(r.d[k], i), c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = k < 3 ? step4_last_shifted(x[k], kShift[k]) : step4_next(x[k], 0u, c);
+    return xor3(x[0], x[1], x[2]) ^ x[3];
+}
+
 template <bool CRCIN>
 __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base, uint64_t stride,
                                                 uint64_t nitems, const uint4 *__restrict__ img,
@@ -152,66 +174,87 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     const uint64_t glast = gend - 1;
     auto item_of = [&](uint64_t gi) { return gi * IPW + g; };
 
-    K1Regs ra, rb;
-    // Uniform step base + per-lane offset: no 64-bit VGPR address math at the
-    // top of a step.  A wave's last prefetch runs one step past its last
-    // group; it re-reads that group (just loaded) -- clamping every wave to
-    // the batch's last group made 4096 waves read the same 8 KiB at the end
-    // of the launch.  The sched_barrier keeps the loads at the top of the
-    // step: left alone, the scheduler sinks them into the chains and the
-    // next step waits on loads issued moments before.
-    auto ld = [&](K1Regs &r, uint64_t gi) {
+    // The loads run three half-steps ahead: a ring of four half-buffers (the
+    // registers of two whole steps), so while one half is checksummed the
+    // next three (12 KiB per wave) are in flight.  Uniform step base +
+    // per-lane offset: no 64-bit VGPR address math at the top of a step.  A
+    // wave's last prefetches run past its last group; they re-read that group
+    // (just loaded) -- clamping every wave to the batch's last group made 4096
+    // waves read the same 8 KiB at the end of the launch.  The sched_barrier
+    // keeps the loads where they are issued: left alone, the scheduler sinks
+    // them into the chains and the next half waits on loads issued moments
+    // before.
+    auto ldh = [&](K1Half &r, uint64_t gi, int q) {
         const uint64_t gu = gi < gend ? gi : glast;
         const uint64_t first = gu * IPW;
         const uint8_t *wb = base + first * stride;
         const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
         // crc_in first: it is consumed before the first chain step, and
-        // vmcnt counts in issue order (issued last, it made the step wait for
-        // all of its loads before any chain could start)
-        if constexpr (CRCIN) r.cin = crc_in[first + gl];
-        else r.cin = 0u;
-        r.template load_at<true>(wb, gl * (uint32_t)stride + li * kK1LaneBytes);
+        // vmcnt counts in issue order
+        if (q == 0) {
+            if constexpr (CRCIN) r.cin = crc_in[first + gl];
+            else r.cin = 0u;
+        }
+        const uint32_t loff = gl * (uint32_t)stride + li * kK1LaneBytes + 4u * kK1Piece * (uint32_t)q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r.d[k] = ld16_nt(wb + loff + k * kK1Piece);
         __builtin_amdgcn_sched_barrier(0);
     };
     // lane 0 XORs ~crc_in into the item's first dword (a register seeded
     // with ~crc_in, crc32c.c:166)
-    auto part0 = [&](K1Regs &m) {
+    auto half0 = [&](K1Half &m) {
         if (li == 0) m.d[0].x ^= ~m.cin;
-        return reduce_level<0>(k1_lane_value(m, c), (lane & 1u) == 0u);
+        return apply_op<4>(kAuxSpanFold, k1_half_value(m, c));
+    };
+    auto part0 = [&](uint32_t u0, K1Half &m1) {
+        return reduce_level<0>(u0 ^ k1_half_value(m1, c), (lane & 1u) == 0u);
+    };
+    K1Half h0, h1, h2, h3;
+    // Step k's halves live in h0/h1 (k even) or h2/h3 (k odd).  Before step k
+    // is checksummed, its two halves and step k + 1's first are issued; each
+    // half's checksum is preceded by the issue of the half three later.
+    const uint64_t nsteps = gend - grp;
+    ldh(h0, grp, 0);
+    ldh(h1, grp, 1);
+    ldh(h2, grp + 1, 0);
+    // (even step k at grp: h0/h1 -> issue h3 (k+1, B), h0 (k+2, A))
+    auto step_even = [&](uint64_t s) {
+        ldh(h3, s + 1, 1);
+        const uint32_t u0 = half0(h0);
+        ldh(h0, s + 2, 0);
+        return part0(u0, h1);
+    };
+    auto step_odd = [&](uint64_t s) {
+        ldh(h1, s + 1, 1);
+        const uint32_t u0 = half0(h2);
+        ldh(h2, s + 2, 0);
+        return part0(u0, h3);
     };
     // One exit, at the bottom of each loop: a break between the halves would
     // give the loop header a second (un-waited) predecessor, and the waitcnt
     // pass would then drain every prefetched load there.
-    const uint64_t nsteps = gend - grp;
-    ld(ra, grp);
     uint64_t k = 0;
     for (; k + 4 <= nsteps; k += 4) {
-        ld(rb, grp + 1);
-        const uint32_t va = part0(ra);
-        ld(ra, grp + 2);
-        const uint32_t vb = part0(rb);
+        const uint32_t va = step_even(grp);
+        const uint32_t vb = step_odd(grp + 1);
         const uint32_t vab = group_pair_level1(va, vb, lane);
-        ld(rb, grp + 3);
-        const uint32_t vc = part0(ra);
-        ld(ra, grp + 4);
-        const uint32_t vd = part0(rb);
+        const uint32_t vc = step_even(grp + 2);
+        const uint32_t vd = step_odd(grp + 3);
         const uint32_t raw = group_reduce32_quad_span(vab, group_pair_level1(vc, vd, lane), lane);
         const uint64_t item = item_of(grp + (li & 3u));
         if (li < 4 && item < nitems) out[item] = ~raw;
         grp += 4;
     }
     for (; k + 2 <= nsteps; k += 2) {
-        ld(rb, grp + 1);
-        const uint32_t va = part0(ra);
-        ld(ra, grp + 2);
-        const uint32_t vb = part0(rb);
+        const uint32_t va = step_even(grp);
+        const uint32_t vb = step_odd(grp + 1);
         const uint32_t raw = group_reduce32_pair_span(va, vb, lane);
         const uint64_t item = item_of(li == 0 ? grp : grp + 1);
         if (li < 2 && item < nitems) out[item] = ~raw;
         grp += 2;
     }
     if (nsteps & 1) {
-        uint32_t v = part0(ra);
+        uint32_t v = step_even(grp);
         v = reduce_level<1>(v, (lane & 3u) == 0u);
         v = reduce_level<2>(v, (lane & 7u) == 0u);
         v = reduce_level<3>(v, (lane & 15u) == 0u);
