@@ -178,16 +178,19 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
     // registers of two whole steps), so while one half is checksummed the
     // next three (12 KiB per wave) are in flight.  Uniform step base +
     // per-lane offset: no 64-bit VGPR address math at the top of a step.  A
-    // wave's last prefetches run past its last group; they re-read that group
-    // (just loaded) -- clamping every wave to the batch's last group made 4096
-    // waves read the same 8 KiB at the end of the launch.  The sched_barrier
-    // keeps the loads where they are issued: left alone, the scheduler sinks
-    // them into the chains and the next half waits on loads issued moments
-    // before.
+    // wave's last prefetches run past its last group; they read the table
+    // image instead (in L2 since every workgroup copied it; their results are
+    // not used): re-reading the wave's last group fetched it from HBM again
+    // (non-temporal loads), 0.7 % of the launch's bytes, and clamping every
+    // wave to the batch's last group made 4096 waves read the same 8 KiB at
+    // the end of the launch.  The sched_barrier keeps the loads where they
+    // are issued: left alone, the scheduler sinks them into the chains and
+    // the next half waits on loads issued moments before.
     auto ldh = [&](K1Half &r, uint64_t gi, int q) {
-        const uint64_t gu = gi < gend ? gi : glast;
+        const bool real = gi < gend;  // (wave-uniform)
+        const uint64_t gu = real ? gi : glast;
         const uint64_t first = gu * IPW;
-        const uint8_t *wb = base + first * stride;
+        const uint8_t *wb = real ? base + first * stride : reinterpret_cast<const uint8_t *>(img);
         const uint32_t gl = first + g < nitems ? g : (uint32_t)(nitems - 1 - first);
         // crc_in first: it is consumed before the first chain step, and
         // vmcnt counts in issue order
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
             if constexpr (CRCIN) r.cin = crc_in[first + gl];
             else r.cin = 0u;
         }
-        const uint32_t loff = gl * (uint32_t)stride + li * kK1LaneBytes + 4u * kK1Piece * (uint32_t)q;
+        const uint32_t loff = (real ? gl * (uint32_t)stride : g * kK1Bytes) + li * kK1LaneBytes + 4u * kK1Piece * (uint32_t)q;
 #pragma unroll
         for (int k = 0; k < 4; ++k) r.d[k] = ld16_nt(wb + loff + k * kK1Piece);
         __builtin_amdgcn_sched_barrier(0);
@@ -2075,8 +2078,11 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
         }
         r_t = p_nt ? step4_next(x, 0u, c) : 0u;
     };
-    // Loads of step s (< ns, else a repeat of the run's last step, whose
-    // result is not used) into b: its window and its status.  K1's layout
+    // Loads of step s into b: its window and its status.  Past the run
+    // (s >= ns: the prefetch of the run's last step, whose result is not
+    // used) the window is the workgroup's zero slot, in L2: a repeat of the
+    // run's last window fetched it from HBM again (non-temporal loads), one
+    // step in 1 + nsr, 3 % of config 5's bytes.  K1's layout
     // and policy (round 5): lane li holds the window's 16-B pieces at
     // 512 k + 16 li, each instruction reads whole lines, non-temporal (the
     // window's lines are read by nothing else: the heads and tails lie
@@ -2087,8 +2093,9 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
         const int src = (int)(2 * min(s, ns - 1) + g);
         const uint64_t lo = (uint32_t)__shfl((int)eglo, src, 64), hi = (uint32_t)__shfl((int)eghi, src, 64);
         b.st = (uint32_t)__shfl((int)est, src, 64);
-        gbyte *blk = ((b.st & kStFused) ? gb + (lo | (hi << 32)) : gz) + 16 * li;
-        const bool z7 = (b.st & kSt31) && li >= 24u;  // piece 7 past B (the window's last line): zeros
+        const bool real = s < ns;  // (wave-uniform)
+        gbyte *blk = ((b.st & kStFused) && real ? gb + (lo | (hi << 32)) : gz) + 16 * li;
+        const bool z7 = (b.st & kSt31) && real && li >= 24u;  // piece 7 past B (the window's last line): zeros
 #pragma unroll
         for (int k = 0; k < (int)kK1Pieces - 1; ++k) b.d.d[k] = ld16_nt(blk + k * kK1Piece);
         b.d.d[kK1Pieces - 1] = ld16_nt(z7 ? gz + 16 * li : blk + (kK1Pieces - 1) * kK1Piece);
