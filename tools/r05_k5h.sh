@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 5: K5 (k_lines) on K1's ring of four half-step buffers (loads three
+# half-steps ahead; ab/k5h = the working tree) against the committed build
+# (ab/head).  GPU parity first.
+#   bash tools/r05_k5h.sh OUT ROUNDS
+source tools/gpu_guard.sh
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r05k5h}; R=${2:-2}; mkdir -p $O
+run 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+tail -1 $O/pytest.log
+grep -q " passed" $O/pytest.log && ! grep -q "failed" $O/pytest.log || { echo "tests failed, stopping"; exit 1; }
+for r in $(seq 1 $R); do
+  for n in head k5h; do
+    for w in "config5 --pages 300" "stamp --pages 300" "config2r"; do
+      echo "== round $r lib $n workload $w" >> $O/ab.txt
+      MCRC_LIB=ab/$n/libmcrc32c.so run 300 python bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline >> $O/ab.txt 2>> $O/ab.err
+    done
+  done
+done
+echo done
