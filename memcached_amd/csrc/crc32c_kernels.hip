@@ -1435,7 +1435,14 @@ __device__ __forceinline__ void put_unit(UnitRec *units, const Balance &b, uint6
 // Per tile (kPlanTile spans, thread-contiguous as k_plan_tiles): the tile's
 // prefix from k_plan_scan plus the exclusive scan inside the tile places every
 // span's units (p0), first block (b0) and, for a one-block span, its slot in
-// the compacted list fastidx (k_blocks).
+// the compacted list fastidx (k_blocks).  The units of a wave's spans are
+// written by the whole wave (round 5): unit q of the wave's inline units
+// goes to lane q mod 64, which finds its span by a search over the lanes'
+// inclusive unit counts -- a span of 16 segments used to take 16 serial
+// make_unit / put_unit rounds in its lane while the wave's other lanes
+// idled.  A span's units after its first are whole segments, so unit j's
+// first block is b0 + (j ? nb0 + 16 (j - 1) : 0), nb0 = the span's blocks
+// less 16 (ns - 1).  tests/test_span_balance.py restates the placement.
 __global__ __launch_bounds__(kPlanThreads) void k_expand(const uint8_t *base, const uint64_t *nunit, const uint8_t *fast,
                                                         const PlanSum *tile_pre, const PlanSum *total, const uint4 *irec,
                                                         uint64_t n, const uint32_t *dn, UnitRec *units, uint64_t cap,
@@ -1444,9 +1451,13 @@ __global__ __launch_bounds__(kPlanThreads) void k_expand(const uint8_t *base, co
                                                         uint32_t *starts) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     __shared__ PlanSum sh[kPlanThreads / 64];
+    // the wave's spans' unit and block bases, slot 64 k + lane
+    __shared__ uint64_t wp0[kPlanThreads / 64][64 * kPlanPer], wb0[kPlanThreads / 64][64 * kPlanPer];
     if (dn) n = *dn;
     const uint64_t ntiles = (n + kPlanTile - 1) / kPlanTile;
     const Balance bal = balance_of(total, n, groups, starts);
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t inline_max = dn ? kExpandInlineDn : kExpandInline;
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint64_t i0 = t * kPlanTile + (uint64_t)threadIdx.x * kPlanPer;
         uint64_t ck[kPlanPer];
@@ -1460,34 +1471,71 @@ __global__ __launch_bounds__(kPlanThreads) void k_expand(const uint8_t *base, co
         }
         PlanSum tot;
         PlanSum pre = plan_add(tile_pre[t], block_scan_excl(s, sh, &tot));
-        for (uint32_t k = 0; k < kPlanPer && i0 + k < n; ++k) {
+        uint32_t cnt[kPlanPer];  // units this lane's span k leaves to the wave
+#pragma unroll
+        for (uint32_t k = 0; k < kPlanPer; ++k) {
             const uint64_t i = i0 + k;
             const uint64_t p0 = pre.units, ns = (uint32_t)ck[k], b0 = pre.blocks;
-            if (fk[k]) fastidx[pre.fast] = (uint32_t)i;
-            const uint4 r = irec[i];
-            const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
-            const bool sane = !(r.y & kInsane);
-            if (p0 + ns <= cap) {
-                const uint32_t s0 = first_seg(base + off, r.z, (uint32_t)ns);
-                if (ns > (dn ? kExpandInlineDn : kExpandInline)) {
-                    big[atomicAdd(nbig, 1u)] = make_uint4((uint32_t)i, (uint32_t)p0, (uint32_t)b0, (uint32_t)(b0 >> 32));
-                } else {
-                    uint64_t bs = b0;
-                    for (uint32_t sg = 0; sg < ns; ++sg) {
-                        const UnitRec u = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, s0 + sg);
-                        put_unit(units, bal, p0 + sg, bs, u);
-                        bs += u.b.z >> 8;
+            cnt[k] = 0;
+            wp0[w][64 * k + lane] = p0;
+            wb0[w][64 * k + lane] = b0;
+            if (i < n) {
+                if (fk[k]) fastidx[pre.fast] = (uint32_t)i;
+                if (p0 + ns <= cap) {
+                    if (ns > inline_max) {
+                        big[atomicAdd(nbig, 1u)] = make_uint4((uint32_t)i, (uint32_t)p0, (uint32_t)b0, (uint32_t)(b0 >> 32));
+                    } else {
+                        cnt[k] = (uint32_t)ns;
                     }
+                    // the last span whose units fit: the record count
+                    if (i + 1 == n || p0 + ns + (uint32_t)nunit[i + 1] > cap)
+                        *nvalid = (uint32_t)(p0 + ns + cuts_before(bal, b0 + (ck[k] >> 32)));
+                } else {
+                    // (one unit with the span's head rule: the same grid, so the same G1)
+                    const uint4 r = irec[i];
+                    const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
+                    whole[atomicAdd(nwhole, 1u)] = make_unit(base, off, r.z, r.w, !(r.y & kInsane), (uint32_t)i, kWhole);
                 }
-                // the last span whose units fit: the record count
-                if (i + 1 == n || p0 + ns + (uint32_t)nunit[i + 1] > cap)
-                    *nvalid = (uint32_t)(p0 + ns + cuts_before(bal, b0 + (ck[k] >> 32)));
-            } else {
-                // (one unit with the span's head rule: the same grid, so the same G1)
-                whole[atomicAdd(nwhole, 1u)] = make_unit(base, off, r.z, r.w, sane, (uint32_t)i, kWhole);
             }
             pre = plan_add(pre, plan_of(ck[k], fk[k]));
         }
+        // the wave's inline units, one per lane and round
+        const uint32_t c = cnt[0] + cnt[1];
+        static_assert(kPlanPer == 2, "two spans per lane below");
+        uint32_t inc = c;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= d) inc += v;
+        }
+        const uint32_t T = (uint32_t)__shfl((int)inc, 63, 64), excl = inc - c;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (wp0 / wb0 written above)
+        for (uint32_t q0 = 0; q0 < T; q0 += 64u) {
+            const uint32_t q = q0 + lane;
+            // owner lane: the first whose inclusive count exceeds q
+            uint32_t o = 0;
+#pragma unroll
+            for (uint32_t step = 32; step; step >>= 1)
+                if ((uint32_t)__shfl((int)inc, (int)(o + step - 1u), 64) <= q) o += step;
+            const uint32_t oe = (uint32_t)__shfl((int)excl, (int)o, 64);
+            const uint32_t oc0 = (uint32_t)__shfl((int)cnt[0], (int)o, 64);
+            if (q < T) {
+                const uint32_t r0 = q - oe;
+                const uint32_t k = r0 < oc0 ? 0u : 1u;
+                const uint32_t j = r0 - (k ? oc0 : 0u);
+                const uint64_t i = t * kPlanTile + (uint64_t)((threadIdx.x & ~63u) + o) * kPlanPer + k;
+                const uint64_t p0 = wp0[w][64 * k + o], b0 = wb0[w][64 * k + o];
+                const uint64_t cki = nunit[i];
+                const uint32_t ns = (uint32_t)cki;
+                const uint4 r = irec[i];
+                const uint64_t off = r.x | ((uint64_t)(r.y & ~kInsane) << 32);
+                const uint32_t s0 = first_seg(base + off, r.z, ns);
+                const uint64_t nb0 = (cki >> 32) - (uint64_t)(kSegBytes / kBlockBytes) * (ns - 1);
+                const uint64_t bs = b0 + (j ? nb0 + (uint64_t)(j - 1) * (kSegBytes / kBlockBytes) : 0u);
+                put_unit(units, bal, p0 + j, bs, make_unit(base, off, r.z, r.w, !(r.y & kInsane), (uint32_t)i, s0 + j));
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (before the next tile rewrites wp0 / wb0)
     }
 }
 
