@@ -46,6 +46,18 @@ def test_span_blocks_is_the_units_niters(seed):
                                  3 * SEG + 123, int(rng.integers(0, 5 * SEG))]))
         assert span_blocks(p, length) == sum(u[2] for u in units_of(0, p, length)), (p, length)
         assert span_units(p, length) == len(units_of(0, p, length))
+        # k_expand's unit placement without a running sum (round 5: a wave's
+        # lanes write any unit of the wave's spans): units after the first are
+        # whole segments, so unit j's first block is
+        # b0 + (j ? nb0 + 16 (j - 1) : 0), nb0 = span_blocks - 16 (ns - 1)
+        units = units_of(0, p, length)
+        ns = len(units)
+        if ns:
+            nb0 = span_blocks(p, length) - (SEG // BLOCK) * (ns - 1)
+            bs = 0
+            for j, u in enumerate(units):
+                assert bs == (nb0 + (SEG // BLOCK) * (j - 1) if j else 0), (p, length, j)
+                bs += u[2]
 
 
 @pytest.mark.parametrize("groups", [1, 2, 3, 7, 64, 1000, 5000])
