@@ -583,31 +583,43 @@ __device__ __forceinline__ bool one_block(const uint8_t *p, uint32_t len, const 
 // - otherwise Z = M_{len+t}(~c ^ raw(F_h)): raw(F_h) = raw of the head
 //   piece's first kh bytes moved to its top (leading zeros leave a zero
 //   register unchanged).
-// One thread.
-// Z when the kernel's R covers the pieces [ph, Ea) as they lie (the third
-// case above; also k_count's wave-cooperative whole spans, whole_chunks).
-__device__ __forceinline__ uint32_t span_corr_pieces(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
-                                                     const uint32_t *xp) {
+// One thread.  (`pieces`: the third case whatever the head -- k_count's
+// wave-cooperative whole spans, whole_chunks, whose R covers [ph, Ea).)
+//
+// Z as a register y to be moved up by N bytes: Z = M_N(y).  Every case of
+// span_corr is of this form, so a wave whose spans take different cases
+// (a head fragment taken or not) runs the multiply by x^(8N) once, not once
+// per case (round 5: in k_count the divergent cases each ran theirs).
+struct CorrArg {
+    uint32_t y;
+    uint64_t N;
+};
+__device__ __forceinline__ CorrArg span_corr_arg(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
+                                                 bool pieces) {
     const uint32_t t = grid_pad(p, len);
-    const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
-    uint32_t y = ~c;
-    if (kh) y ^= raw16(shl_bytes(ld_piece(p - kh), 16 - kh), t8);  // raw(F_h)
-    return mulmodp_dev(y, xpow8_dev(xp, (uint64_t)len + t));
+    if (len == 0) return {~c, t};
+    const uint64_t vlen = (uint64_t)len + t;
+    const SpanHead h = span_head(p, len);
+    if (pieces || !h.drop) {
+        // the kernel's R covers the pieces [ph, Ea): y = ~c ^ raw(F_h), N = len + t
+        const uint32_t kh = (uint32_t)((uintptr_t)p & 15u);
+        uint32_t y = ~c;
+        if (kh) y ^= raw16(shl_bytes(ld_piece(p - kh), 16 - kh), t8);  // raw(F_h)
+        return {y, vlen};
+    }
+    // the head fragment [p, G1) is the thread's; G1 = Ea: the whole span,
+    // whose register moves up by t
+    const bool all = h.g1o == vlen;
+    return {reg_advance(~c, p, all ? len : (uint32_t)h.g1o, t8), all ? (uint64_t)t : vlen - h.g1o};
+}
+__device__ __forceinline__ uint32_t corr_apply(const CorrArg &z, const Tab8 &t8, const uint32_t *xp) {
+    // (one block, every one-block span: a table step)
+    return z.N == kBlockBytes ? t8.block(z.y) : mulmodp_dev(z.y, xpow8_dev(xp, z.N));
 }
 __device__ __forceinline__ uint32_t span_corr(const uint8_t *p, uint32_t len, uint32_t c, const Tab8 &t8,
                                               const uint32_t *xp) {
-    const uint32_t t = grid_pad(p, len);
-    if (len == 0) return mulmodp_dev(~c, xp[t]);
-    const uint64_t vlen = (uint64_t)len + t;
-    const SpanHead h = span_head(p, len);
-    if (h.drop && h.g1o == vlen) return mulmodp_dev(reg_advance(~c, p, len, t8), xp[t]);
-    if (!h.drop) return span_corr_pieces(p, len, c, t8, xp);
-    // Ea - G1 is whole blocks; one block (every one-block span) is a table step
-    const uint32_t r = reg_advance(~c, p, (uint32_t)h.g1o, t8);
-    return vlen - h.g1o == kBlockBytes ? t8.block(r) : mulmodp_dev(r, xpow8_dev(xp, vlen - h.g1o));
+    return corr_apply(span_corr_arg(p, len, c, t8, false), t8, xp);
 }
-
-
 
 // Item header fields (memcached.h:613-636) from bytes 28..43 of the image at
 // it, read as the two aligned pieces holding them (every byte of those pieces
@@ -1128,8 +1140,8 @@ __device__ __forceinline__ void count_item(const SpanArgs &a, uint64_t i, const 
     uint32_t z = 0;
     if (it.sane) {
         // (a whole span's R from the wave, whole_chunks: z = R ^ Z of its pieces)
-        z = whole ? rwhole ^ span_corr_pieces(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow)
-                  : span_corr(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, a.xpow);
+        z = corr_apply(span_corr_arg(it.p, it.len, MODE == 0 ? it.aux : 0u, t8, whole), t8, a.xpow) ^
+            (whole ? rwhole : 0u);
         if (MODE == 1) z ^= mulmodp_dev(~it.aux, a.xpow[grid_pad(it.p, it.len)]);  // W
     }
     irec[i] = make_uint4((uint32_t)off, (uint32_t)(off >> 32) | (it.sane ? 0u : kInsane), it.len, z);
