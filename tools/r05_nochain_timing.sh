@@ -1,0 +1,13 @@
+#!/bin/bash
+source tools/gpu_guard.sh
+export TMPDIR=/tmp
+O=gpurun_out/r05nc; mkdir -p $O
+for r in 1 2; do
+  for n in head nochain; do
+    for w in "config5 --pages 300" "config2r"; do
+      echo "== round $r lib $n workload $w" >> $O/ab.txt
+      MCRC_LIB=ab/$n/libmcrc32c.so run 300 python bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline >> $O/ab.txt 2>> $O/ab.err
+    done
+  done
+done
+echo done
