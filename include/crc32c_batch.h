@@ -161,7 +161,9 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
  * kernels are enqueued on `stream` (the caller fences reads of the wbuf on
  * that stream).  ok (optional) marks stamped images;
  * malformed images are left untouched and counted in *nbad.  region_bytes as
- * for crc32c_verify_items. */
+ * for crc32c_verify_items.  Images are expected not to overlap (extstore
+ * packs them back to back); where one image's span covers another's exptime,
+ * its CRC may or may not include that image's new stamp. */
 int crc32c_stamp_items(void *base, uint64_t base_bytes, uint64_t region_bytes,
                        const uint64_t *item_offsets, uint64_t n, uint8_t *ok, uint64_t *nbad,
                        unsigned flags, void *stream);

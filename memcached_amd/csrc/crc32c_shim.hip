@@ -90,6 +90,11 @@ struct Device {
     uint32_t *nfb = nullptr;    // k_lines' fallback count (device)
     uint32_t *route = nullptr;  // k_census's verdict: K5 (1) or the planned path (0)
     hipStream_t stream = nullptr, copy = nullptr;
+    // a stamp's k_fix runs on `side` beside the damaged images' planned path
+    // (fork: after k_lines on the caller's stream; join: the caller's stream
+    // waits for it before the call's last kernel)
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};  // host-batch pipeline slots
     std::mutex mu;              // serialises the entry points that use the scratch below
@@ -281,6 +286,9 @@ int init_device(Device &d, int id) {
     d.route = d.nfb + 1;
     HIP_OK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_OK(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&d.fork, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&d.join, hipEventDisableTiming));
     HIP_OK(hipEventCreate(&d.ev0));
     HIP_OK(hipEventCreate(&d.ev1));
     HIP_OK(hipEventCreateWithFlags(&d.busy, hipEventDisableTiming));
@@ -606,9 +614,19 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     hipLaunchKernelGGL(mcrc_dev::k_census<MODE>, dim3(1), dim3(mcrc_dev::kCensus), 0, st, a, d.route);
     launch_k5<MODE, true>(d, a, io, st);
     const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 1024);
-    if (MODE == 2)
-        hipLaunchKernelGGL(mcrc_dev::k_fix, dim3(g), dim3(256), 0, st, a, (const uint2 *)io.rt,
+    if (MODE == 2) {
+        // k_fix (the stamps of the images k_lines checksummed) on the side
+        // stream, beside the planned path of the images it listed: its
+        // scattered partial-sector writes and that path's small launches
+        // overlap.  They touch disjoint bytes unless images overlap
+        // (crc32c_batch.h: then an image's CRC may or may not see another
+        // image's new stamp).
+        HIP_OK(hipEventRecord(d.fork, st));
+        HIP_OK(hipStreamWaitEvent(d.side, d.fork, 0));
+        hipLaunchKernelGGL(mcrc_dev::k_fix, dim3(g), dim3(256), 0, d.side, a, (const uint2 *)io.rt,
                            (const uint32_t *)d.route);
+        HIP_OK(hipEventRecord(d.join, d.side));
+    }
     hipLaunchKernelGGL(mcrc_dev::k_gather_offs, dim3(g), dim3(256), 0, st, a.offsets, (const uint32_t *)io.fb,
                        (const uint32_t *)d.nfb, fo, (const uint32_t *)d.route);
     HIP_OK(hipGetLastError());
@@ -618,6 +636,7 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     f.dn = d.nfb;  // (f.n = n: the list's upper bound)
     f.ok = want_ok ? fok : nullptr;
     int rc = launch_units<MODE>(d, f, st, Path{});
+    if (MODE == 2) HIP_OK(hipStreamWaitEvent(st, d.join, 0));  // (also when the planned path failed)
     if (rc) return rc;
     if (want_ok)
         hipLaunchKernelGGL(mcrc_dev::k_scatter_ok, dim3(g), dim3(256), 0, st, (const uint8_t *)fok,

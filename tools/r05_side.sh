@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round 5: a stamp's k_fix on a side stream beside the damaged images'
+# planned path (ab/side = the working tree) against the committed build
+# (ab/head).  GPU parity first, then stamp / config 5 timings and a stamp
+# kernel trace per build.
+#   bash tools/r05_side.sh OUT ROUNDS
+source tools/gpu_guard.sh
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r05sd}; R=${2:-3}; mkdir -p $O
+run 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+tail -1 $O/pytest.log
+grep -q " passed" $O/pytest.log && ! grep -q "failed" $O/pytest.log || { echo "tests failed, stopping"; exit 1; }
+for r in $(seq 1 $R); do
+  for n in head side; do
+    for w in "stamp --pages 300" "config5 --pages 300"; do
+      echo "== round $r lib $n workload $w" >> $O/ab.txt
+      MCRC_LIB=ab/$n/libmcrc32c.so run 300 python bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline >> $O/ab.txt 2>> $O/ab.err
+    done
+  done
+done
+for n in head side; do
+  MCRC_LIB=ab/$n/libmcrc32c.so run 300 rocprofv3 --kernel-trace --stats -d $O/kt_$n -o kt --output-format csv -- python3 bench.py --workload stamp --pages 300 --steps 5 --warmup 1 --no-cpu-baseline > $O/kt_$n.json 2> $O/kt_$n.err
+done
+echo done
