@@ -505,10 +505,13 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
             hipLaunchKernelGGL((mcrc_dev::k_spans<false>), dim3(grid), dim3(mcrc_dev::kSpanBlock),
                                mcrc_dev::kLdsImageK1Bytes, st, x, d.img);
     };
-    const int g1 = (int)std::min<uint64_t>((n + 255) / 256, 4096);
+    const int g1 = (int)std::min<uint64_t>((n + 255) / 256, 2048);
     // k_final: 1024 workgroups (it adds its bad count once per workgroup: 4096
     // groups cost 30 us of same-address atomics per 4.8 M verified items, 64 Ki
-    // groups 190 us); k_count: 4096 (1024 measured 25 % slower on config 3).
+    // groups 190 us); k_count: 2048 (round 5: config 3 and the mixed pages
+    // 0.2-1.2 % faster than 4096, 1024 no better and config 5 +1.3 %;
+    // profiles/r05_ablations/k_count_grid_ab.txt; round 4 measured 1024 25 %
+    // slower than 4096 on config 3 before the whole spans went wave-wide).
     const int gf = (int)std::min<uint64_t>((n + 255) / 256, 1024);
     if (path.small) {
         if (path.host_counted) {
