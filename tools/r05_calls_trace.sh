@@ -1,0 +1,6 @@
+#!/bin/bash
+source tools/gpu_guard.sh
+export TMPDIR=/tmp
+O=gpurun_out/r05calls; mkdir -p $O
+run 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 bench.py --workload calls > $O/calls.json 2> $O/calls.err
+echo done
