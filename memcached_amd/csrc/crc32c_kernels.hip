@@ -14,6 +14,10 @@
 //     k_final<MODE 2> stamps it (the spill CRC of storage.c:567, batched per
 //     wbuf).  k_walk walks the pages on the device.
 // K4  k_blocks: spans whose unit is one 4 KiB block (K1's loop, gathered).
+// K5  k_lines<MODE>: spans or item images whose span is one 4 KiB window of
+//     whole lines after a short head (every 4165-B image of config 5 and the
+//     config-2 variant), each image's header, head and tail done once by one
+//     lane of a run of consecutive images; k_fix stamps (MODE 2).
 //     k_small: batches of up to 8192 spans in one launch (IO batches, wbufs,
 //     the coalescing queue).
 //
@@ -26,8 +30,9 @@ namespace mcrc_dev {
 // K1: fixed-length aligned items
 // ===========================================================================
 
-// 16-B load of item bytes.  (Non-temporal loads: K1 reads through ld16_nt,
-// see k_fixed; they were 5-11 % worse for the span kernels in round 1.)
+// 16-B load of item bytes.  (The streaming reads of K1, K5 and the span
+// kernels use ld16_nt below, since round 5 on whole lines; non-temporal
+// loads of 16-B anchored blocks were 5-11 % worse in round 1.)
 __device__ __forceinline__ uint4 ld16(const void *p) { return *reinterpret_cast<const uint4 *>(p); }
 // Global-memory byte and piece pointers.  k_lines keeps its addresses in
 // these: derived from the kernel arguments through generic pointers, they
@@ -1706,7 +1711,7 @@ __global__ __launch_bounds__(1024) void k_small(SpanArgs a, const uint4 *__restr
     const uint32_t R = group_reduce32_span(acc, lane);
     uint32_t nb = 0;
     if (valid) {
-        // Z (span_corr, no fragment): M_{len+t}(~c ^ raw(F_h)) ^ raw(F_t)
+        // Z on k_small's own 16-B grid (its blocks keep F_t): M_{len+t}(~c ^ raw(F_h)) ^ raw(F_t)
         const uint32_t cin = MODE == 0 ? it.aux : 0u;
         uint32_t z = mulmodp_dev(~cin, a.xpow[t]);  // (len 0: R = 0, crc = c)
         if (len) {

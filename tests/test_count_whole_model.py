@@ -1,5 +1,5 @@
 """CPU restatement of k_count's wave-cooperative whole spans (round 4,
-crc32c_kernels.hip whole_chunks / span_corr_pieces).
+crc32c_kernels.hip whole_chunks / span_corr_arg's pieces case).
 
 A span D = [p, E) of vlen = len + t <= kWholeMax bytes is all its thread's
 (span_corr: z = M_t(f), f the register after D from ~c).  Its lane no longer
