@@ -543,7 +543,10 @@ __device__ __forceinline__ uint32_t reg_advance(uint32_t r, const uint8_t *p, ui
 // per 16 B, so long fragments cost more than the block step they save --
 // DESIGN.md section 3.)
 constexpr uint32_t kFragMax = 128;    // a head fragment [p, G1) of at most this
-constexpr uint32_t kWholeMax = 1024;  // a whole span of vlen at most this
+// (512 since round 5: 256-512 beat 1024 by 1.0-1.3 % on the mixed pages and
+// matched it on config 3; 2048 / 3072 were 1-3 % slower --
+// profiles/r05_ablations/whole_span_limit_ab.txt)
+constexpr uint32_t kWholeMax = 512;   // a whole span of vlen at most this
 static_assert(kWholeMax + kGridAlign <= kBlockBytes, "a whole span held by its thread is its own fragment (G1 = Ea)");
 // Is the head fragment (G1 - p = g1o) the span thread's?  For vlen <= kWholeMax
 // the fragment is the whole span (G1 = Ea).

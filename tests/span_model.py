@@ -7,7 +7,7 @@ SEG = 64 * 1024
 BLOCK = 4096
 WHOLE = 0xFFFFFFFF
 FRAG_MAX = 128    # kFragMax: a head fragment [p, G1) of at most this is the thread's
-WHOLE_MAX = 1024  # kWholeMax: so is a whole span of vlen at most this
+WHOLE_MAX = 512   # kWholeMax: so is a whole span of vlen at most this
 POLY = 0x82F63B78
 M32 = 0xFFFFFFFF
 
