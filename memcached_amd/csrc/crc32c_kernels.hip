@@ -5,7 +5,7 @@
 //     Replaces N calls of crc32c(0, item, len), crc32c_hw (crc32c.c:161-246)
 //     reached from storage.c:567.
 // K2  k_spans<UNITS>: any offsets, lengths and alignment; one 32-lane group
-//     per work unit of <= 64 KiB (configs 3 and 5, storage.c:172 read-back
+//     per work unit of <= 128 KiB (configs 3 and 5, storage.c:172 read-back
 //     spans), then k_final<MODE 0> per span.
 // K3  the same kernels over the spans of packed item images in extstore
 //     pages, [off+32, off+ITEM_ntotal) (k_count<MODE 1/2> parses the
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 // exclusive scan -> k_expand; a batch whose spans all fit one unit uses unit
 // u = span u directly.  Segment units shift their value into place and XOR it
 // into the span's accumulator:
-//   R(span) = sum_s M_{64 KiB * (nseg-1-s)}(R(segment s)),
+//   R(span) = sum_s M_{kSegBytes * (nseg-1-s)}(R(segment s)),
 // then k_final turns R into the CRC (or the verdict) of every span.
 //
 // Unit geometry (the K1 geometry: CH = 32, LPI = 32): a unit [p, e), e
@@ -319,7 +319,10 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
 
 constexpr uint32_t kRowBytes = 1024;  // a row: two of K1's 512-B piece rows (the head-block skip)
 constexpr uint32_t kBlockBytes = 4 * kRowBytes;  // 4096
-constexpr uint32_t kSegBytes = 64 * 1024;  // (16-256 KiB measured; 24-64 KiB alike)
+// (round 5: 128 KiB; config 3 -1.1..-1.3 % against 64 KiB in two sessions, the
+// mixed pages and config 5 within noise, 256 KiB like 128 --
+// profiles/r05_ablations/segment_size_ab.txt; rounds 1-3 found 24-64 KiB alike)
+constexpr uint32_t kSegBytes = 128 * 1024;
 // Longest span (CRC32C_MAX_SPAN): a unit's grid offsets (eo, G - p, the block
 // count times 4 KiB) are 32-bit and signed, and a span that overlaps others
 // past the plan's capacity is one unit.  Twice the largest item memcached
@@ -698,7 +701,7 @@ __device__ __forceinline__ ItemDesc fetch_item(const SpanArgs &a, uint64_t i) {
 // Work-unit record written by k_expand (32 B, one dwordx4 pair per unit):
 //   a = {offset of the unit's first byte from base (lo, hi), e - p, E - p}
 //   b = {z (the span's item record), span index, flags | niters << 8,
-//        4 KiB blocks from e to the span's end: 16 (nseg - 1 - segment), more for a piece}
+//        4 KiB blocks from e to the span's end: (kSegBytes / 4 KiB) (nseg - 1 - segment), more for a piece}
 struct alignas(16) UnitRec {
     uint4 a, b;
 };
@@ -1461,8 +1464,9 @@ __device__ __forceinline__ void put_unit(UnitRec *units, const Balance &b, uint6
 // inclusive unit counts -- a span of 16 segments used to take 16 serial
 // make_unit / put_unit rounds in its lane while the wave's other lanes
 // idled.  A span's units after its first are whole segments, so unit j's
-// first block is b0 + (j ? nb0 + 16 (j - 1) : 0), nb0 = the span's blocks
-// less 16 (ns - 1).  tests/test_span_balance.py restates the placement.
+// first block is b0 + (j ? nb0 + S (j - 1) : 0), nb0 = the span's blocks
+// less S (ns - 1), S = kSegBytes / 4 KiB.  tests/test_span_balance.py
+// restates the placement.
 __global__ __launch_bounds__(kPlanThreads) void k_expand(const uint8_t *base, const uint64_t *nunit, const uint8_t *fast,
                                                         const PlanSum *tile_pre, const PlanSum *total, const uint4 *irec,
                                                         uint64_t n, const uint32_t *dn, UnitRec *units, uint64_t cap,

@@ -3,7 +3,7 @@ per-span correction (memcached_amd/csrc/crc32c_kernels.hip: nseg_of,
 span_head, span_units, make_unit, load_block, span_corr).  Test
 infrastructure: the CPU tests check the addressing and the algebra with it,
 without a GPU."""
-SEG = 64 * 1024
+SEG = 128 * 1024  # kSegBytes
 BLOCK = 4096
 WHOLE = 0xFFFFFFFF
 FRAG_MAX = 128    # kFragMax: a head fragment [p, G1) of at most this is the thread's

@@ -34,7 +34,7 @@ def random_spans(rng, n, maxlen):
         pos += int(rng.integers(0, 40))
         spans.append((pos, int(length)))
         pos += int(length)
-    return spans, pos + 64
+    return spans, pos + 256  # (slack past the last span: its grid ends up to 127 B after it)
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -49,7 +49,7 @@ def test_span_blocks_is_the_units_niters(seed):
         # k_expand's unit placement without a running sum (round 5: a wave's
         # lanes write any unit of the wave's spans): units after the first are
         # whole segments, so unit j's first block is
-        # b0 + (j ? nb0 + 16 (j - 1) : 0), nb0 = span_blocks - 16 (ns - 1)
+        # b0 + (j ? nb0 + S (j - 1) : 0), nb0 = span_blocks - S (ns - 1), S = SEG / BLOCK
         units = units_of(0, p, length)
         ns = len(units)
         if ns:
