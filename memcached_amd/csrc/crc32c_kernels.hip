@@ -2026,22 +2026,24 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
     const uint64_t waves = blockDim.x >> 6;
     const uint64_t W = gridDim.x * waves;
     const uint64_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)waves + (threadIdx.x >> 6));
-    // Runs: wave w checksums the contiguous chunk [w C, (w + 1) C) of images
-    // (C = ceil(n / W) rounded up to even), as a first run of 1 + (w % nsr)
-    // steps and then runs of nsr steps: the same work on every wave, the
-    // waves' run starts spread over nsr steps, and a wave's consecutive runs
-    // read consecutive lines (config 5 -2.5 %, configs 2r / stamp within
-    // noise, against round k of wave w being the run from (k W + w) 2 nsr:
-    // profiles/r04_ablations/k5_lines_chunk_ab.txt).  (Staggering only the
-    // first runs of the round-robin order unbalanced the waves and was 1-9 %
-    // slower: profiles/r04_ablations/k5_lines_stagger_ab.txt.)
+    // Runs, dealt round robin (round 5): run k of wave w is the images
+    // [(k W + w) 2 nsr, +2 nsr), so at any time the waves' windows lie
+    // within W runs (~1 GB at 4165-B images) of each other.  Round 4 gave
+    // each wave a contiguous chunk of ceil(n / W) images with staggered
+    // first runs (-2.5 % at 300 pages); at 1000 pages (67 GB) those 4096
+    // streams, 16 MB apart, ran 3.5-7 % slower per page than 300 pages did,
+    // and the round-robin order took config 5 at 1000 pages from
+    // 11.32-11.76 to 10.92-10.93 ms, 300 pages and config 2r level or better
+    // (profiles/r05_ablations/k5_run_order_ab.txt).
     // tests/test_items_lines_model.py checks that the runs cover every image
     // exactly once.
-    const uint64_t C = ((n + W - 1) / W + 1) & ~1ull;
-    const uint64_t f0 = 1 + w0 % nsr, cend = min((w0 + 1) * C, n);
-    auto run_start = [&](uint64_t k) -> uint64_t { return w0 * C + (k == 0 ? 0 : 2 * (f0 + (k - 1) * nsr)); };
-    auto run_steps = [&](uint64_t k) -> uint64_t { return k == 0 ? f0 : nsr; };
-    if ((uint64_t)blockIdx.x * waves * C >= n) return;
+    const uint64_t cend = n;
+    auto run_start = [&](uint64_t k) -> uint64_t { return (k * W + w0) * run_imgs; };
+    auto run_steps = [&](uint64_t k) -> uint64_t {
+        (void)k;
+        return nsr;
+    };
+    if ((uint64_t)blockIdx.x * waves * run_imgs >= n) return;
     if (MODE != 0 && io.route && *io.route == 0) {  // the census sent the batch to the planned path
         if (blockIdx.x == 0 && threadIdx.x == 0) *io.nfb = (uint32_t)n;
         return;

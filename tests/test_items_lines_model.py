@@ -151,36 +151,32 @@ def test_line_anchored_shapes():
 
 
 def lines_runs(n, W, w, nsr):
-    """The images [(start, steps), ...] of wave w's runs (k_lines, chunked)."""
-    C = ((n + W - 1) // W + 1) & ~1
-    f0, cend = 1 + w % nsr, min((w + 1) * C, n)
+    """The images [(start, steps), ...] of wave w's runs (k_lines, round
+    robin: run k of wave w starts at image (k W + w) 2 nsr)."""
     runs, k = [], 0
     while True:
-        start = w * C + (0 if k == 0 else 2 * (f0 + (k - 1) * nsr))
-        if start >= cend:
+        start = (k * W + w) * 2 * nsr
+        if start >= n:
             return runs
-        steps = min(f0 if k == 0 else nsr, (cend - start + 1) // 2)
-        runs.append((start, steps))
+        runs.append((start, min(nsr, (n - start + 1) // 2)))
         k += 1
 
 
 @pytest.mark.parametrize("n", [1, 2, 63, 4096, 4097, 65535, 1 << 20, 4833600])
 @pytest.mark.parametrize("grid", [1, 7, 256, 1024])
 def test_line_runs_cover_every_image_once(n, grid):
-    """Every image is taken by exactly one lane of one step of one run, runs
-    hold at most 2 nsr <= 64 images (one per lane) and every wave's share is
-    at most C images; nsr as launch_k5 (crc32c_shim.hip) sets it."""
+    """Every image is taken by exactly one lane of one step of one run and
+    runs hold at most 2 nsr <= 64 images (one per lane); nsr as launch_k5
+    (crc32c_shim.hip) sets it."""
     W = grid * 16
     nsr = min(32, max(1, (n + 2 * W - 1) // (2 * W)))
     seen = np.zeros(n, dtype=np.int32)
-    C = ((n + W - 1) // W + 1) & ~1
     for w in range(W):
-        if w * C >= n:
+        if w * 2 * nsr >= n:
             break
-        runs = lines_runs(n, W, w, nsr)
-        for start, steps in runs:
+        for start, steps in lines_runs(n, W, w, nsr):
             assert 1 <= steps <= nsr
             lanes = np.arange(64)
-            items = start + lanes[(lanes < 2 * steps) & (start + lanes < min((w + 1) * C, n))]
+            items = start + lanes[(lanes < 2 * steps) & (start + lanes < n)]
             seen[items] += 1
     assert (seen == 1).all()
