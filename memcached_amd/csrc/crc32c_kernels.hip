@@ -363,8 +363,9 @@ struct SpanArgs {
     const uint32_t *nunits;    // device-side unit count
     uint32_t *span_acc;        // planned batches: R per span (segment units XOR their shifted values in)
     const uint32_t *segpow;    // rows k (x^i * x^(8 * 4096 * k), i < 32) for k < kSegpowLo, then k = kSegpowLo j
-    const uint32_t *starts;    // balanced plan: group g's records are [starts[g], starts[g + 1])
+    const uint32_t *starts;    // balanced plan: share v's records are [starts[v], starts[v + 1])
                                // (0xffffffff: *nunits); nullptr: round robin over units
+    uint32_t rounds;           // balanced plan: group g takes shares g, G + g, .. (rounds of them)
     uint64_t region;           // MODE 1: items never cross a multiple of `region` (0: no bound)
     uint32_t cfl;              // MODE 1/2: bytes of the ITEM_CFLAGS suffix, sizeof(client_flags_t):
                                // 4, or 8 in a LARGE_CLIENT_FLAGS build (memcached.h:96-100)
@@ -979,12 +980,21 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
     c.lane4hi = c.lane4 | 0x10000u;
     const uint64_t ngroups_total = (uint64_t)gridDim.x * (blockDim.x >> 5);
     const uint32_t g = g0 + ((threadIdx.x >> 6) << 1) + (lane >> 5);
+    // Rounds (round 5): the balanced plan cuts the batch's blocks into
+    // rounds x G equal shares in block order and group g takes shares g,
+    // G + g, 2G + g, ..., so the groups stream through one round's range of
+    // the batch (about 8 GiB: crc32c_shim.hip plan_rounds) at a time instead
+    // of each through its own 1/G of all of it.  Each round restarts the
+    // group's pipeline.
+    const uint32_t nrounds = bal ? a.rounds : 1u;
     uint64_t u = g;
-    uint64_t ub = nunits;  // the group's records end here
-    if (bal) {
-        u = g ? min(a.starts[g], (uint32_t)nunits) : 0u;
-        ub = min(a.starts[g + 1], (uint32_t)nunits);
-    }
+    uint64_t ub = nunits;  // the group's records (of this round) end here
+    auto share = [&](uint32_t rd) {
+        const uint64_t v = (uint64_t)rd * ngroups_total + g;
+        u = v ? min(a.starts[v], (uint32_t)nunits) : 0u;
+        ub = min(a.starts[v + 1], (uint32_t)nunits);
+    };
+    if (bal) share(0);
     const uint64_t ustep = bal ? 1u : ngroups_total;
 
     UnitDesc cur = decode_unit<UNITS>(a, fetch_unit<UNITS>(a, u, ub, li), u, nunits, lane);
@@ -1091,17 +1101,33 @@ __global__ __launch_bounds__(kSpanBlock) void k_spans(SpanArgs a, const uint4 *_
         }
     };
 
-    // nothing issued before the loop stays pending into it (the waitcnt pass
-    // would otherwise wait for it, vmcnt(0), at the top of every iteration)
-    __builtin_amdgcn_s_waitcnt(0);
-    // One, wave-uniform exit at the bottom (a group that has finished runs
-    // empty steps until the other has): a divergent or mid-loop exit gives the
-    // loop header an un-waited predecessor, and the waitcnt pass then drains
-    // the prefetch there (vmcnt(0)) on every iteration.
-    for (;;) {
-        step(w0, w1);
-        step(w1, w0);
-        if (!__builtin_amdgcn_readfirstlane(__any(cur.valid()))) break;
+    for (uint32_t rd = 0;;) {
+        // nothing issued before the loop stays pending into it (the waitcnt
+        // pass would otherwise wait for it, vmcnt(0), at the top of every
+        // iteration)
+        __builtin_amdgcn_s_waitcnt(0);
+        // One, wave-uniform exit at the bottom (a group that has finished
+        // runs empty steps until the other has): a divergent or mid-loop exit
+        // gives the loop header an un-waited predecessor, and the waitcnt
+        // pass then drains the prefetch there (vmcnt(0)) on every iteration.
+        for (;;) {
+            step(w0, w1);
+            step(w1, w0);
+            if (!__builtin_amdgcn_readfirstlane(__any(cur.valid()))) break;
+        }
+        if (++rd >= nrounds) break;
+        // (a round whose first share is empty is followed by empty ones: a
+        // small plan -- K5's fallback list -- fills round 0 or less)
+        if (a.starts[(uint64_t)rd * ngroups_total] >= (uint32_t)nunits) break;
+        // the next round's share: a fresh pipeline (the ring and the block
+        // prefetch of the finished share hold nothing of it)
+        share(rd);
+        cur = decode_unit<UNITS>(a, fetch_unit<UNITS>(a, u, ub, li), u, nunits, lane);
+        ring = fetch_unit<UNITS>(a, u + (1 + (li >> 3)) * ustep, ub, li);
+        sl = 0;
+        k = 0;
+        acc = 0;
+        load_block(w0, cur, 0, li, zero);
     }
 }
 

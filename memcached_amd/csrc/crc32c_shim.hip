@@ -363,6 +363,17 @@ bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 // A/B baseline, profiles/r03_ablations/k2_balanced_plan_ab.jsonl).
 constexpr bool kSpanBalance = true;
 uint32_t span_groups(const Device &d) { return (uint32_t)d.cus * (mcrc_dev::kSpanBlock / 32); }
+// Rounds of the balanced plan (k_spans): one per kRoundBytes of the batch's
+// buffer, at most kMaxRounds, so the span kernel's groups stream through
+// about 8 GiB of it at a time (round 5: the mixed pages at 300 pages -2 % in
+// three sessions, config 3 and 1000 pages within noise; 1-4 GiB rounds'
+// pipeline restarts cost as much as their locality gained at 1000 pages;
+// profiles/r05_ablations/plan_rounds_ab.txt).
+constexpr uint64_t kRoundBytes = 8ull << 30;
+constexpr uint32_t kMaxRounds = 16;
+uint32_t plan_rounds(const mcrc_dev::SpanArgs &a) {
+    return (uint32_t)std::min<uint64_t>(kMaxRounds, std::max<uint64_t>(1, (a.base_bytes + kRoundBytes - 1) / kRoundBytes));
+}
 
 int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
     if (d.plan_items < n) {
@@ -390,13 +401,14 @@ int ensure_plan(Device &d, uint64_t n, uint64_t cap) {
     if (d.plan_units < cap) {
         (void)hipFree(d.units);
         d.plan_units = 0;
-        // (+ one record per group boundary of the balanced plan)
-        if (hipMalloc(&d.units, (cap + span_groups(d)) * sizeof(mcrc_dev::UnitRec)) != hipSuccess)
+        // (+ one record per share boundary of the balanced plan)
+        if (hipMalloc(&d.units, (cap + (uint64_t)kMaxRounds * span_groups(d)) * sizeof(mcrc_dev::UnitRec)) != hipSuccess)
             return CRC32C_ENOMEM;
         d.plan_units = cap;
     }
     if (!d.counters && hipMalloc(&d.counters, 16) != hipSuccess) return CRC32C_ENOMEM;
-    if (!d.starts && hipMalloc(&d.starts, (span_groups(d) + 1) * 4) != hipSuccess) return CRC32C_ENOMEM;
+    if (!d.starts && hipMalloc(&d.starts, ((uint64_t)kMaxRounds * span_groups(d) + 1) * 4) != hipSuccess)
+        return CRC32C_ENOMEM;
     return CRC32C_OK;
 }
 
@@ -552,7 +564,10 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     if (rc) return rc;
     uint32_t *nvalid = d.counters, *nwhole = d.counters + 1, *nbig = d.counters + 2;
     HIP_OK(hipMemsetAsync(nvalid, 0, 12, st));  // nvalid, nwhole, nbig
-    if (kSpanBalance) HIP_OK(hipMemsetAsync(d.starts, 0xff, (span_groups(d) + 1) * 4, st));
+    // the balanced plan's shares: rounds x the span kernel's groups
+    const uint32_t rounds = kSpanBalance ? plan_rounds(a) : 1u;
+    const uint32_t shares = rounds * span_groups(d);
+    if (kSpanBalance) HIP_OK(hipMemsetAsync(d.starts, 0xff, ((uint64_t)shares + 1) * 4, st));
     a.span_acc = d.span_acc;
     if (!path.counted)
         hipLaunchKernelGGL((mcrc_dev::k_count<MODE>), dim3(g1), dim3(256), 0, st, a, d.nunit, d.irec, d.fast);
@@ -571,16 +586,17 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
     hipLaunchKernelGGL(mcrc_dev::k_expand, dim3(gt), dim3(mcrc_dev::kPlanThreads), 0, st, a.base,
                        (const uint64_t *)d.nunit, (const uint8_t *)d.fast, (const mcrc_dev::PlanSum *)d.tile_pre,
                        (const mcrc_dev::PlanSum *)total, (const uint4 *)d.irec, n, a.dn, d.units, cap, nvalid, d.whole,
-                       nwhole, d.big, nbig, d.fastidx, span_groups(d), starts);
+                       nwhole, d.big, nbig, d.fastidx, shares, starts);
     hipLaunchKernelGGL(mcrc_dev::k_expand_big, dim3(1024), dim3(256), 0, st, a.base, (const uint64_t *)d.nunit,
                        (const mcrc_dev::PlanSum *)total, (const uint4 *)d.irec, d.units, (const uint4 *)d.big,
-                       (const uint32_t *)nbig, n, a.dn, span_groups(d), starts);
+                       (const uint32_t *)nbig, n, a.dn, shares, starts);
     mcrc_dev::SpanArgs u = a;
     u.units = d.units;
     u.nunits = nvalid;
     u.span_acc = d.span_acc;
     u.segpow = d.segpow;
     u.starts = starts;
+    u.rounds = rounds;
     // spans whose unit is one whole block: k_blocks over the compacted list;
     // the other spans' units: the span kernel
     hipLaunchKernelGGL((mcrc_dev::k_blocks<false, true>), dim3(grid_for(d, n)), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st,

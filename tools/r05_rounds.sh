@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 5: the balanced plan in rounds (ab/rounds = the working tree: one
+# round of G shares per 2 GiB of the buffer, group g takes shares g, G + g,
+# ..) against one share per group (ab/head).  Full GPU suite first.
+#   bash tools/r05_rounds.sh OUT ROUNDS
+source tools/gpu_guard.sh
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r05rd}; R=${2:-2}; mkdir -p $O
+run 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+tail -1 $O/pytest.log
+grep -q " passed" $O/pytest.log && ! grep -q "failed" $O/pytest.log || { echo "tests failed, stopping"; exit 1; }
+for r in $(seq 1 $R); do
+  for n in head rounds; do
+    for w in "pagesmix --pages 1000" "pagesmix --pages 300" "config3" "config5 --pages 300"; do
+      echo "== round $r lib $n workload $w" >> $O/ab.txt
+      MCRC_LIB=ab/$n/libmcrc32c.so run 300 python bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline >> $O/ab.txt 2>> $O/ab.err
+    done
+  done
+done
+echo done
