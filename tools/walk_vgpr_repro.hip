@@ -24,7 +24,9 @@
 //   P32     P24 at 32 VGPRs;
 //   PS24    P24 over pages whose images all sit at one alignment (16 page
 //           sets, one per sh = (p + 28) & 15): which alignments go wrong;
-//   PS32    PS24 at 32 VGPRs.
+//   PS32    PS24 at 32 VGPRs;
+//   PSA     PS24 with the header taken by v_alignbyte_b32 instead of 64-bit
+//           shifts (parse_hdr_alignbyte: 19 VGPRs, allocated 24).
 // For the wrong wbufs of T24 the host replays the same lane-parallel walk and
 // prints the first round trip that differs: the kernel's state and lane m's
 // parsed fields against the header bytes at the pointer that state implies.
@@ -52,6 +54,7 @@ using namespace mcrc_dev;
     } while (0)
 
 constexpr int kRounds = 4, kTr = 8;  // traced round trips per wbuf, dwords per round trip
+constexpr int kAbVgprs = 19;         // k_parse<0, true, true>'s count in this build (allocated: 24)
 
 template <int CLOB, bool TRACE, bool REV = false>
 __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t nw, uint32_t *cnt, uint32_t *trace) {
@@ -119,7 +122,29 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
 // The parse alone (no walk state, no readlane): every lane parses the header
 // of image r * 64 + j of its wave's wbuf, as the walk's lanes do, and checks
 // nbytes / nkey against byte loads of the same image.
-template <int CLOB, bool LAYOUT = false>
+// parse_hdr without 64-bit shifts: the 16 header bytes from the two pieces'
+// dwords with v_alignbyte_b32 (byte funnel of two dwords)
+__device__ __forceinline__ ItemHdr parse_hdr_alignbyte(const uint8_t *it) {
+    const uint32_t sh = (uint32_t)((uintptr_t)(it + 28) & 15u);
+    const uint8_t *q = it + 28 - sh;
+    const bool two = sh + 13 >= 16;
+    const Piece v0 = ld_piece(q), v1 = ld_piece(q + (two ? 16 : 0));
+    const uint32_t d[8] = {(uint32_t)v0.lo, (uint32_t)(v0.lo >> 32), (uint32_t)v0.hi, (uint32_t)(v0.hi >> 32),
+                           two ? (uint32_t)v1.lo : 0u, two ? (uint32_t)(v1.lo >> 32) : 0u,
+                           two ? (uint32_t)v1.hi : 0u, two ? (uint32_t)(v1.hi >> 32) : 0u};
+    const uint32_t qi = sh >> 2, b = sh & 3u;
+    uint32_t w[5];
+#pragma unroll
+    for (uint32_t m = 0; m < 5; ++m)
+        w[m] = qi == 0 ? d[m] : qi == 1 ? d[m + 1] : qi == 2 ? d[m + 2] : d[m + 3];
+    // out[m] = image bytes 28 + 4m .. 31 + 4m
+    const uint32_t o1 = __builtin_amdgcn_alignbyte(w[2], w[1], b), o2 = __builtin_amdgcn_alignbyte(w[3], w[2], b),
+                   o3 = __builtin_amdgcn_alignbyte(w[4], w[3], b);
+    (void)w[0];
+    return {__builtin_amdgcn_alignbyte(w[1], w[0], b), o1, (o2 >> 16) & 0xffffu, (o3 >> 8) & 0xffu};
+}
+
+template <int CLOB, bool LAYOUT = false, bool AB = false>
 __global__ __launch_bounds__(64 * kWalkWaves) void k_parse(SpanArgs a, uint64_t nw, uint32_t *cnt) {
     if (CLOB == 32) asm volatile("" ::: "v31");
     const uint32_t j = threadIdx.x & 63u;
@@ -132,7 +157,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_parse(SpanArgs a, uint64_t 
             const uint32_t i = r * 64u + j;
             if (i >= (LAYOUT ? 1000u : 1007u)) break;
             const uint8_t *p = wb + (uint64_t)i * (LAYOUT ? 4176u : 4165u);
-            const ItemHdr h = parse_hdr(p);
+            const ItemHdr h = AB ? parse_hdr_alignbyte(p) : parse_hdr(p);
             // every image here has nbytes < 2^20 (4098, at most one bit of 0..19
             // flipped) and nkey 10 or 0; the walk's wrong parses gave
             // nbytes 0x0a111002 or nkey 105 (checking against byte loads of
@@ -372,15 +397,18 @@ int main(int argc, char **argv) {
     {
         const uint32_t per = 1000, stride = 4176;
         SpanArgs b = a;
-        for (int cl = 24; cl <= 32; cl += 8) {
-            printf("PS%d: wrong parses of %llu by sh = (p + 28) & 15:", cl, (unsigned long long)nwb * per);
+        for (int cl = 24; cl <= 40; cl += 8) {  // (40: PSA, the v_alignbyte parse at its own allocation)
+            if (cl == 40) printf("PSA (parse_hdr_alignbyte, %d VGPRs): wrong parses of %llu by sh = (p + 28) & 15:", kAbVgprs,
+                                 (unsigned long long)nwb * per);
+            else printf("PS%d: wrong parses of %llu by sh = (p + 28) & 15:", cl, (unsigned long long)nwb * per);
             for (uint32_t phase = 0; phase < 16; ++phase) {
                 CHECK(hipMemset(d, 0x5a, bytes));
                 hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, d, nwb, wbuf, 777u + phase, per, stride, phase);
                 b.base = d + phase;  // (the last wbuf's images end 4176 B short of the pages' end)
                 CHECK(hipMemset(cnt, 0, 4));
                 if (cl == 24) hipLaunchKernelGGL((k_parse<24, true>), dim3(gw), dim3(64 * kWalkWaves), 0, 0, b, nwb, cnt);
-                else hipLaunchKernelGGL((k_parse<32, true>), dim3(gw), dim3(64 * kWalkWaves), 0, 0, b, nwb, cnt);
+                else if (cl == 32) hipLaunchKernelGGL((k_parse<32, true>), dim3(gw), dim3(64 * kWalkWaves), 0, 0, b, nwb, cnt);
+                else hipLaunchKernelGGL((k_parse<0, true, true>), dim3(gw), dim3(64 * kWalkWaves), 0, 0, b, nwb, cnt);
                 CHECK(hipDeviceSynchronize());
                 uint32_t nbad = 0;
                 CHECK(hipMemcpy(&nbad, cnt, 4, hipMemcpyDeviceToHost));
