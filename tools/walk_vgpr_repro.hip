@@ -20,13 +20,15 @@
 //           the original order, separated;
 //   R32     R24 at 32 VGPRs;
 //   P24     the parse alone (k_parse: every lane parses its images' headers
-//           and checks them against byte loads, no walk state), 24 VGPRs;
+//           against the values the fill gives, no walk state), 24 VGPRs;
 //   P32     P24 at 32 VGPRs;
 //   PS24    P24 over pages whose images all sit at one alignment (16 page
 //           sets, one per sh = (p + 28) & 15): which alignments go wrong;
 //   PS32    PS24 at 32 VGPRs;
 //   PSA     PS24 with the header taken by v_alignbyte_b32 instead of 64-bit
-//           shifts (parse_hdr_alignbyte: 19 VGPRs, allocated 24).
+//           shifts (parse_hdr_alignbyte: 19 VGPRs, allocated 24);
+//   PSAP    PSA with 5 loaded values held live across the loop, so that the
+//           allocation's top registers are in use (24 VGPRs).
 // For the wrong wbufs of T24 the host replays the same lane-parallel walk and
 // prints the first round trip that differs: the kernel's state and lane m's
 // parsed fields against the header bytes at the pointer that state implies.
@@ -55,6 +57,7 @@ using namespace mcrc_dev;
 
 constexpr int kRounds = 4, kTr = 8;  // traced round trips per wbuf, dwords per round trip
 constexpr int kAbVgprs = 19;         // k_parse<0, true, true>'s count in this build (allocated: 24)
+constexpr int kAbPad = 5, kAbPadVgprs = 24;  // PSAP: pad values, k_parse<0, true, true, kAbPad>'s count
 
 template <int CLOB, bool TRACE, bool REV = false>
 __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t nw, uint32_t *cnt, uint32_t *trace) {
@@ -119,9 +122,6 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
     }
 }
 
-// The parse alone (no walk state, no readlane): every lane parses the header
-// of image r * 64 + j of its wave's wbuf, as the walk's lanes do, and checks
-// nbytes / nkey against byte loads of the same image.
 // parse_hdr without 64-bit shifts: the 16 header bytes from the two pieces'
 // dwords with v_alignbyte_b32 (byte funnel of two dwords)
 __device__ __forceinline__ ItemHdr parse_hdr_alignbyte(const uint8_t *it) {
@@ -144,12 +144,24 @@ __device__ __forceinline__ ItemHdr parse_hdr_alignbyte(const uint8_t *it) {
     return {__builtin_amdgcn_alignbyte(w[1], w[0], b), o1, (o2 >> 16) & 0xffffu, (o3 >> 8) & 0xffu};
 }
 
-template <int CLOB, bool LAYOUT = false, bool AB = false>
+// The parse alone (no walk state, no readlane): every lane parses the header
+// of image r * 64 + j of its wave's wbuf, as the walk's lanes do, and checks
+// nbytes / nkey against the values the fill gives (LAYOUT: the one-alignment
+// pages; AB: parse_hdr_alignbyte; PAD: values held live across the loop).
+template <int CLOB, bool LAYOUT = false, bool AB = false, int PAD = 0>
 __global__ __launch_bounds__(64 * kWalkWaves) void k_parse(SpanArgs a, uint64_t nw, uint32_t *cnt) {
     if (CLOB == 32) asm volatile("" ::: "v31");
     const uint32_t j = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t bad = 0;
+    // PAD values loaded before and used after the loop: live across every
+    // parse, they fill the allocation up to its top registers
+    uint32_t pad[PAD > 0 ? PAD : 1];
+#pragma unroll
+    for (int m = 0; m < PAD; ++m) {
+        pad[m] = reinterpret_cast<const uint32_t *>(a.base)[m * 64 + j];
+        asm volatile("" : "+v"(pad[m]));
+    }
     for (uint64_t w = (uint64_t)blockIdx.x * kWalkWaves + wave; w < nw; w += (uint64_t)gridDim.x * kWalkWaves) {
         const uint8_t *wb = a.base + w * a.region;
 #pragma unroll 1
@@ -164,6 +176,11 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_parse(SpanArgs a, uint64_t 
             // the image instead takes the kernel to 26-27 VGPRs)
             bad += (h.nbytes >> 20 != 0u) | (h.nkey != 10u && h.nkey != 0u);
         }
+    }
+#pragma unroll
+    for (int m = 0; m < PAD; ++m) {
+        asm volatile("" : "+v"(pad[m]));
+        bad += pad[m] == 0x13572468u;  // (never: the pages hold no such word)
     }
     if (bad) atomicAdd(cnt, bad);
 }
@@ -397,8 +414,10 @@ int main(int argc, char **argv) {
     {
         const uint32_t per = 1000, stride = 4176;
         SpanArgs b = a;
-        for (int cl = 24; cl <= 40; cl += 8) {  // (40: PSA, the v_alignbyte parse at its own allocation)
-            if (cl == 40) printf("PSA (parse_hdr_alignbyte, %d VGPRs): wrong parses of %llu by sh = (p + 28) & 15:", kAbVgprs,
+        for (int cl = 24; cl <= 48; cl += 8) {  // (40: PSA, the v_alignbyte parse at its own allocation; 48: PSAP)
+            if (cl == 48) printf("PSAP (PSA with %d values live across the loop: %d VGPRs): wrong parses of %llu by sh:", kAbPad,
+                                 kAbPadVgprs, (unsigned long long)nwb * per);
+            else if (cl == 40) printf("PSA (parse_hdr_alignbyte, %d VGPRs): wrong parses of %llu by sh = (p + 28) & 15:", kAbVgprs,
                                  (unsigned long long)nwb * per);
             else printf("PS%d: wrong parses of %llu by sh = (p + 28) & 15:", cl, (unsigned long long)nwb * per);
             for (uint32_t phase = 0; phase < 16; ++phase) {
@@ -408,7 +427,8 @@ int main(int argc, char **argv) {
                 CHECK(hipMemset(cnt, 0, 4));
                 if (cl == 24) hipLaunchKernelGGL((k_parse<24, true>), dim3(gw), dim3(64 * kWalkWaves), 0, 0, b, nwb, cnt);
                 else if (cl == 32) hipLaunchKernelGGL((k_parse<32, true>), dim3(gw), dim3(64 * kWalkWaves), 0, 0, b, nwb, cnt);
-                else hipLaunchKernelGGL((k_parse<0, true, true>), dim3(gw), dim3(64 * kWalkWaves), 0, 0, b, nwb, cnt);
+                else if (cl == 40) hipLaunchKernelGGL((k_parse<0, true, true>), dim3(gw), dim3(64 * kWalkWaves), 0, 0, b, nwb, cnt);
+                else hipLaunchKernelGGL((k_parse<0, true, true, kAbPad>), dim3(gw), dim3(64 * kWalkWaves), 0, 0, b, nwb, cnt);
                 CHECK(hipDeviceSynchronize());
                 uint32_t nbad = 0;
                 CHECK(hipMemcpy(&nbad, cnt, 4, hipMemcpyDeviceToHost));
