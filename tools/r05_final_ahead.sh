@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round 5: k_final with four spans' loads issued ahead (ab/fin) against the
+# committed build (ab/head): the planned-path GPU tests on ab/fin, then
+# alternating batches of the mixed pages and config 3, and a kernel trace of
+# the mixed pages with each library.
+#   bash tools/r05_final_ahead.sh OUT ROUNDS
+source tools/gpu_guard.sh
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r05fa}; R=${2:-3}; mkdir -p $O
+MCRC_LIB=ab/fin/libmcrc32c.so run 900 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider -k "planned or config3 or pages or stamp or verify or spans or items" > $O/pytest.log 2>&1
+tail -1 $O/pytest.log
+grep -q " passed" $O/pytest.log && ! grep -q "failed" $O/pytest.log || { echo "tests failed, stopping"; exit 1; }
+for r in $(seq 1 $R); do
+  for n in head fin; do
+    for w in "pagesmix --pages 300" "config3"; do
+      echo "== round $r lib $n workload $w" >> $O/ab.txt
+      MCRC_LIB=ab/$n/libmcrc32c.so run 300 python bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline >> $O/ab.txt 2>> $O/ab.err
+    done
+  done
+done
+for n in head fin; do
+  MCRC_LIB=ab/$n/libmcrc32c.so run 300 rocprofv3 --kernel-trace --stats -d $O/kt_$n -o kt --output-format csv -- python3 bench.py --workload pagesmix --pages 300 --steps 5 --warmup 1 --no-cpu-baseline > $O/kt_$n.json 2> $O/kt_$n.err
+done
+echo done
