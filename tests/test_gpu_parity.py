@@ -333,6 +333,53 @@ def test_stamp_items(torch):
     assert bytes(bad[int(offs[11]) + 28:int(offs[11]) + 32]) == b"\0\0\0\0"
 
 
+def test_item_headers_at_every_alignment(torch):
+    """Item images starting at every offset mod 16, so the header fields the
+    kernels parse from two 16-B pieces (bytes 28..43, funnel-shifted by
+    (off + 28) & 15: parse_hdr) sit at every alignment, with key
+    lengths, value sizes, CAS and client flags varied so that the field bytes
+    differ from image to image: stamp, verify (device and host) and the
+    device page walk agree with the oracle, and one damaged image per
+    alignment is reported exactly."""
+    rng = np.random.default_rng(53)
+    items = []
+    for i in range(2048):
+        nkey = 1 + (i * 37) % 250
+        cas = None if i % 3 == 0 else i + 1
+        cfl = (i * 2654435761) & 0xFFFFFFFF if i % 5 == 0 else 0
+        key = (b"%06d" % i + b"k" * 250)[:nkey]
+        vlen = int(rng.integers(0, 20000))
+        # ITEM_ntotal = 1 (mod 16): consecutive images step through every residue
+        vlen += (1 - len(layout.make_item(key, bytes(vlen), cas=cas, client_flags=cfl))) % 16
+        items.append(layout.make_item(key, rng.integers(0, 256, vlen, dtype=np.uint8).tobytes(), cas=cas,
+                                      client_flags=cfl))
+    wbuf = 1 << 20
+    buf, offs = layout.pack_wbufs(items, wbuf)
+    assert {int(o) % 16 for o in offs} == set(range(16))
+    soffs, slens = layout.spans_of(buf, offs)
+    want = buf.copy()
+    layout.store_crcs(want, offs, oracle.batch(buf, soffs, slens))
+    d = _dev(torch, buf)
+    ok, nbad = mc.stamp_items(d, _dev(torch, offs.view(np.int64)), region_bytes=wbuf)
+    assert nbad == 0 and ok.cpu().numpy().all()
+    np.testing.assert_array_equal(d.cpu().numpy(), want)
+    # one damaged image per start residue (a value byte flipped)
+    victims = [min(i for i in range(16 * r + 16, offs.size) if int(offs[i]) % 16 == r) for r in range(16)]
+    bad = want.copy()
+    for v in victims:
+        o = int(offs[v])
+        bad[o + int(rng.integers(48, layout.ntotal_of(bad, o)))] ^= 0x20
+    for dev in (True, False):
+        ok, nbad = mc.verify_items(_dev(torch, bad) if dev else bad, _dev(torch, offs.view(np.int64)) if dev else offs,
+                                   region_bytes=wbuf)
+        ok = ok.cpu().numpy() if dev else ok
+        assert nbad == len(victims) and sorted(np.flatnonzero(ok == 0).tolist()) == sorted(victims)
+    np.testing.assert_array_equal(_walk(bad, wbuf), offs)
+    got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, bad), wbuf)
+    np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), offs)
+    assert nbad == len(victims) and sorted(np.flatnonzero(got_ok.cpu().numpy() == 0).tolist()) == sorted(victims)
+
+
 def _walk(buf, wbuf):
     """storage_compact_readback's walk (storage.c:950-1070), one read per wbuf."""
     offs = []
