@@ -1,6 +1,6 @@
 // crc32c_kernels.hip -- hand-written gfx950 kernels for batched CRC-32C.
 //
-// K1  k_fixed<CRCIN>: equal 4 KiB, 16-B aligned items at a fixed stride
+// K1  k_fixed<CRCIN, NT>: equal 4 KiB, 16-B aligned items at a fixed stride
 //     (extstore spill batches of one slab class; BASELINE configs 2 and 4).
 //     Replaces N calls of crc32c(0, item, len), crc32c_hw (crc32c.c:161-246)
 //     reached from storage.c:567.
@@ -139,7 +139,10 @@ __device__ __forceinline__ uint32_t k1_half_value(const K1Half &r, const LaneCtx
     return xor3(x[0], x[1], x[2]) ^ x[3];
 }
 
-template <bool CRCIN>
+// NT: non-temporal loads, for a 128-B aligned base and stride (every line
+// whole in one item); otherwise the default policy, so that a line two
+// neighbouring items share is not fetched twice (K1Regs::load_at).
+template <bool CRCIN, bool NT>
 __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base, uint64_t stride,
                                                 uint64_t nitems, const uint4 *__restrict__ img,
                                                 const uint32_t *__restrict__ crc_in,
@@ -205,7 +208,8 @@ __global__ __launch_bounds__(1024) void k_fixed(const uint8_t *__restrict__ base
         }
         const uint32_t loff = (real ? gl * (uint32_t)stride : g * kK1Bytes) + li * kK1LaneBytes + 4u * kK1Piece * (uint32_t)q;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) r.d[k] = ld16_nt(wb + loff + k * kK1Piece);
+        for (int k = 0; k < 4; ++k)
+            r.d[k] = NT ? ld16_nt(wb + loff + k * kK1Piece) : ld16((gbyte *)(wb + loff + k * kK1Piece));
         __builtin_amdgcn_sched_barrier(0);
     };
     // lane 0 XORs ~crc_in into the item's first dword (a register seeded
@@ -647,6 +651,14 @@ struct ItemHdr {
         return 48ull + nkey + 1 + nbytes + ((flags & 256u) ? cfl : 0) + ((flags & 2u) ? 8 : 0);
     }
 };
+//
+// The fields are funnelled out of the pieces' dwords with v_alignbyte_b32, not
+// with 64-bit shifts: a v_lshlrev_b64 whose shift amount sits in the last VGPR
+// of the wave's allocation computes wrongly beside a co-resident wave on
+// gfx950 (tools/shift64_top_vgpr.hip), and the 64-bit funnel
+// this parse used through round 5 put its amount exactly there in a 24-VGPR
+// kernel.  tests/test_kernel_resources.py checks that no kernel of the
+// library, and no instruction of this parse, takes that form.
 template <typename BytePtr>
 __device__ __forceinline__ ItemHdr parse_hdr(BytePtr it) {
     // (pointer arithmetic, not an integer round trip: the loads stay global
@@ -655,12 +667,18 @@ __device__ __forceinline__ ItemHdr parse_hdr(BytePtr it) {
     const BytePtr q = it + 28 - sh;
     const bool two = sh + 13 >= 16;  // byte 41 lies in the next piece
     const Piece v0 = ld_piece(q), v1 = ld_piece(q + (two ? 16 : 0));
-    const uint64_t w0 = v0.lo, w1 = v0.hi, w2 = two ? v1.lo : 0, w3 = two ? v1.hi : 0;
-    const uint64_t a0 = sh < 8 ? w0 : w1, a1 = sh < 8 ? w1 : w2, a2 = sh < 8 ? w2 : w3;
-    const uint32_t k = 8 * (sh & 7u);
-    const uint64_t f0 = k ? (a0 >> k) | (a1 << (64 - k)) : a0;  // image bytes 28..35
-    const uint64_t f1 = k ? (a1 >> k) | (a2 << (64 - k)) : a1;  // 36..43
-    return {(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)(f1 >> 16) & 0xffffu, (uint32_t)(f1 >> 40) & 0xffu};
+    const uint32_t d[8] = {(uint32_t)v0.lo, (uint32_t)(v0.lo >> 32), (uint32_t)v0.hi, (uint32_t)(v0.hi >> 32),
+                           two ? (uint32_t)v1.lo : 0u, two ? (uint32_t)(v1.lo >> 32) : 0u,
+                           two ? (uint32_t)v1.hi : 0u, two ? (uint32_t)(v1.hi >> 32) : 0u};
+    // w[m] = the dword holding image byte 28 + 4m (and the next one's low bytes)
+    const uint32_t qi = sh >> 2, b = sh & 3u;
+    uint32_t w[5];
+#pragma unroll
+    for (uint32_t m = 0; m < 5; ++m) w[m] = qi == 0 ? d[m] : qi == 1 ? d[m + 1] : qi == 2 ? d[m + 2] : d[m + 3];
+    // image bytes 28..31, 32..35, 36..39 (it_flags 38..39), 40..43 (nkey 41)
+    const uint32_t o0 = __builtin_amdgcn_alignbyte(w[1], w[0], b), o1 = __builtin_amdgcn_alignbyte(w[2], w[1], b),
+                   o2 = __builtin_amdgcn_alignbyte(w[3], w[2], b), o3 = __builtin_amdgcn_alignbyte(w[4], w[3], b);
+    return {o0, o1, (o2 >> 16) & 0xffffu, (o3 >> 8) & 0xffu};
 }
 
 // The CRC span of the item image at base + off with header h (parsed when

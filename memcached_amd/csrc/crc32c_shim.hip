@@ -297,8 +297,10 @@ int init_device(Device &d, int id) {
         HIP_OK(hipEventCreateWithFlags(&d.done[k], hipEventDisableTiming));
     }
     const void *k160[] = {
-        (const void *)mcrc_dev::k_fixed<false>,
-        (const void *)mcrc_dev::k_fixed<true>,
+        (const void *)mcrc_dev::k_fixed<false, true>,
+        (const void *)mcrc_dev::k_fixed<true, true>,
+        (const void *)mcrc_dev::k_fixed<false, false>,
+        (const void *)mcrc_dev::k_fixed<true, false>,
         (const void *)mcrc_dev::k_spans<false>,
         (const void *)mcrc_dev::k_spans<true>,
         (const void *)mcrc_dev::k_small<0>,
@@ -541,7 +543,7 @@ int launch_units(Device &d, mcrc_dev::SpanArgs a, hipStream_t st, Path path) {
         return CRC32C_OK;
     }
     if (identity) {
-        // (spans of at most kWholeMax - 15 bytes are all their threads' in k_final)
+        // (spans of at most kWholeMax - (kGridAlign - 1) bytes are all their threads' in k_final)
         if (a.len + mcrc_dev::kGridAlign - 1 > mcrc_dev::kWholeMax) {
             if (one_block_len(a.len) && a.offsets)
                 hipLaunchKernelGGL((mcrc_dev::k_blocks<true, true>), dim3(grid_for(d, n)), dim3(1024),
@@ -633,6 +635,17 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     hipLaunchKernelGGL(mcrc_dev::k_census<MODE>, dim3(1), dim3(mcrc_dev::kCensus), 0, st, a, d.route);
     launch_k5<MODE, true>(d, a, io, st);
     const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 1024);
+    // Once k_fix is forked, every exit joins it back into st, error exits
+    // included: the caller's busy event (recorded on st after this returns)
+    // must cover k_fix's writes to the images and its reads of io.rt.
+    struct Join {
+        hipStream_t st;
+        hipEvent_t ev;
+        bool armed = false;
+        ~Join() {
+            if (armed) (void)hipStreamWaitEvent(st, ev, 0);
+        }
+    } join{st, d.join};
     if (MODE == 2) {
         // k_fix (the stamps of the images k_lines checksummed) on the side
         // stream, beside the planned path of the images it listed: its
@@ -645,6 +658,7 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
         hipLaunchKernelGGL(mcrc_dev::k_fix, dim3(g), dim3(256), 0, d.side, a, (const uint2 *)io.rt,
                            (const uint32_t *)d.route);
         HIP_OK(hipEventRecord(d.join, d.side));
+        join.armed = true;
     }
     hipLaunchKernelGGL(mcrc_dev::k_gather_offs, dim3(g), dim3(256), 0, st, a.offsets, (const uint32_t *)io.fb,
                        (const uint32_t *)d.nfb, fo, (const uint32_t *)d.route);
@@ -655,7 +669,10 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
     f.dn = d.nfb;  // (f.n = n: the list's upper bound)
     f.ok = want_ok ? fok : nullptr;
     int rc = launch_units<MODE>(d, f, st, Path{});
-    if (MODE == 2) HIP_OK(hipStreamWaitEvent(st, d.join, 0));  // (also when the planned path failed)
+    if (MODE == 2) {
+        join.armed = false;
+        HIP_OK(hipStreamWaitEvent(st, d.join, 0));  // (also when the planned path failed)
+    }
     if (rc) return rc;
     if (want_ok)
         hipLaunchKernelGGL(mcrc_dev::k_scatter_ok, dim3(g), dim3(256), 0, st, (const uint8_t *)fok,
@@ -708,13 +725,16 @@ bool k1_shape(const crc32c_spans &s) {
 
 // K1 touches no shared scratch, counter or event of the device: callers may
 // enqueue it without d.mu.
+// Non-temporal loads only when every 128-B line belongs to one item.
 int launch_k1(const Device &d, const crc32c_spans &s, hipStream_t st) {
-    if (s.crc_in)
-        hipLaunchKernelGGL((mcrc_dev::k_fixed<true>), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
-                           st, (const uint8_t *)s.base, s.stride, s.n, d.img, s.crc_in, s.out);
-    else
-        hipLaunchKernelGGL((mcrc_dev::k_fixed<false>), dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes,
-                           st, (const uint8_t *)s.base, s.stride, s.n, d.img, s.crc_in, s.out);
+    const bool nt = ((uintptr_t)s.base & 127u) == 0 && (s.stride & 127u) == 0;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid_for(d, s.n)), dim3(kBlock), mcrc_dev::kLdsImageK1Bytes, st,
+                           (const uint8_t *)s.base, s.stride, s.n, (const uint4 *)d.img, (const uint32_t *)s.crc_in,
+                           s.out);
+    };
+    if (s.crc_in) nt ? go(mcrc_dev::k_fixed<true, true>) : go(mcrc_dev::k_fixed<true, false>);
+    else nt ? go(mcrc_dev::k_fixed<false, true>) : go(mcrc_dev::k_fixed<false, false>);
     HIP_OK(hipGetLastError());
     return CRC32C_OK;
 }

@@ -69,6 +69,82 @@ def test_every_kernel_allocates_at_least_32_vgprs(tmp_path):
             assert v <= 64, (n, v)
 
 
+_SHIFT64 = re.compile(r"\s(v_(?:lshlrev|lshrrev|ashrrev)_[bi]64)\s+(v\[\d+:\d+\]),\s*(\S+),")
+
+
+def _disasm_by_function(co):
+    dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", str(co)], check=True,
+                         capture_output=True, text=True).stdout
+    out, cur = {}, None
+    for line in dis.splitlines():
+        m = re.match(r"[0-9a-f]+ <(\S+)>:$", line)
+        if m:
+            cur = m.group(1)
+            out[cur] = []
+        elif cur:
+            out[cur].append(line)
+    return out
+
+
+def test_no_64bit_shift_takes_its_amount_from_the_top_vgpr(tmp_path):
+    """The named cause of the 24-VGPR header miscompute (DESIGN.md section
+    3.7, tools/shift64_top_vgpr.hip): a 64-bit VALU shift whose amount operand
+    is the last VGPR of the wave's allocation.  No instruction of the library
+    may take that form, whatever the VGPR floor."""
+    co = _code_object(tmp_path)
+    ks = _kernels(co)
+    fns = _disasm_by_function(co)
+    bad, nshift = [], 0
+    for name, (vgpr, _a, _l) in ks.items():
+        top = f"v{((vgpr + 7) // 8) * 8 - 1}"
+        assert name in fns, name
+        for ins in fns[name]:
+            m = _SHIFT64.search(ins)
+            if m:
+                nshift += 1
+                if m.group(3) == top:
+                    bad.append((name, ins.strip()))
+    assert nshift > 0  # (the scan sees the library's shifts)
+    assert not bad, bad
+
+
+def test_parse_hdr_has_no_64bit_shift(tmp_path):
+    """parse_hdr (crc32c_kernels.hip) funnels the header bytes with
+    v_alignbyte_b32: a probe kernel holding only the parse, for both pointer
+    types the library instantiates, has no 64-bit VALU shift."""
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "memcached_amd", "csrc")
+    src = tmp_path / "probe.hip"
+    src.write_text(
+        '#include "crc32c_kernels.hip"\n'
+        "using namespace mcrc_dev;\n"
+        "__global__ void probe_flat(const uint8_t *p, uint32_t *o) {\n"
+        "    const ItemHdr h = parse_hdr(p + threadIdx.x * 13u);\n"
+        "    o[threadIdx.x] = h.exptime ^ h.nbytes * 3u ^ h.flags * 5u ^ h.nkey * 7u;\n"
+        "}\n"
+        "__global__ void probe_global(const uint8_t *p, uint32_t *o) {\n"
+        "    gbyte *g = (gbyte *)p;\n"
+        "    const ItemHdr h = parse_hdr(g + threadIdx.x * 13u);\n"
+        "    o[threadIdx.x] = h.exptime ^ h.nbytes * 3u ^ h.flags * 5u ^ h.nkey * 7u;\n"
+        "}\n")
+    asm = tmp_path / "probe.s"
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", csrc, "--cuda-device-only", "-S",
+                    str(src), "-o", str(asm)], check=True, capture_output=True)
+    # (the include brings the library's own kernels along: only the probes' bodies count)
+    bodies = {}
+    for blk in re.split(r"\n(?=_Z\S*:)", asm.read_text()):
+        m = re.match(r"(_Z\S*probe_\w+?Pj):", blk)
+        if m:
+            bodies[m.group(1)] = blk.split("\t.section")[0]
+    assert len(bodies) == 2, list(bodies)
+    for name, body in bodies.items():
+        assert "v_alignbyte_b32" in body and re.search(r"(global|flat)_load_dwordx4", body), name
+        shifts = [ln.strip() for ln in body.splitlines() if re.search(r"\sv_(lshlrev|lshrrev|ashrrev)_[bi]64\s", ln)]
+        assert not shifts, (name, shifts)
+
+
 def test_no_build_switch_alternatives_in_the_product_sources():
     """One build of the product: no #if/#ifdef feature switch selects an
     untested alternative kernel path (round-4 review item 5)."""

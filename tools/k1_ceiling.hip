@@ -469,9 +469,9 @@ int main(int argc, char **argv) {
     uint4 *dimg_c;
     CHECK(hipMalloc(&dimg_c, img_c.size() * 4));
     CHECK(hipMemcpy(dimg_c, img_c.data(), img_c.size() * 4, hipMemcpyHostToDevice));
-    CHECK(hipFuncSetAttribute((const void *)k_fixed<false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsImageK1Bytes));
+    CHECK(hipFuncSetAttribute((const void *)k_fixed<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsImageK1Bytes));
     auto run_k1 = [&] {
-        hipLaunchKernelGGL((k_fixed<false>), dim3(cus), dim3(1024), kLdsImageK1Bytes, 0, d, kItemBytes, kItems, dimg_c,
+        hipLaunchKernelGGL((k_fixed<false, true>), dim3(cus), dim3(1024), kLdsImageK1Bytes, 0, d, kItemBytes, kItems, dimg_c,
                            nullptr, out);
     };
     // clock settle: 300 ms of K1 launches (not for a counter pass: REPS 1)
