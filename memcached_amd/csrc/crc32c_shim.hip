@@ -181,15 +181,21 @@ struct Device {
 enum { kPinStage, kPinOffs, kPinOk, kPinCrc };
 
 std::mutex g_dev_mu;  // device discovery and first initialisation only
+// Device state by HIP ordinal (every visible device; only gfx950 ones are
+// ever initialised), and the library's device index -> HIP ordinal map: the
+// gfx950 ordinals in order.  crc32c_gpu_count() is that map's size and
+// crc32c_batch_multi's part g runs on HIP ordinal g_gfx[g], so a node whose
+// first ordinals are other parts still shards over its gfx950 devices.
 std::vector<std::unique_ptr<Device>> g_devs;
-int g_ndev = -1;
-// Initialised devices by id, published once (release) after init_device: the
-// per-call lookup reads them without g_dev_mu, so threads driving different
-// devices (crc32c_batch_multi, IO threads on several GPUs) never serialise on
-// a process-wide lock after the first call.
+std::vector<int> g_gfx;
+int g_nhip = -1;
+// Initialised devices by ordinal, published once (release) after init_device:
+// the per-call lookup reads them without g_dev_mu, so threads driving
+// different devices (crc32c_batch_multi, IO threads on several GPUs) never
+// serialise on a process-wide lock after the first call.
 constexpr int kMaxDevices = 64;
 std::atomic<Device *> g_ready[kMaxDevices];
-std::atomic<int> g_ndev_pub{-1};
+std::atomic<int> g_ngfx_pub{-1};
 
 // MCRC_DEBUG=1 in the environment: report the failing HIP call on stderr.
 bool debug_on() {
@@ -205,15 +211,9 @@ bool debug_on() {
         }                                                                                          \
     } while (0)
 
-int count_gfx950() {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-    int good = 0;
-    for (int d = 0; d < n; ++d) {
-        hipDeviceProp_t p;
-        if (hipGetDeviceProperties(&p, d) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ++good;
-    }
-    return good == n ? n : good;  // assume homogeneous nodes
+bool is_gfx950(int ordinal) {
+    hipDeviceProp_t p;
+    return hipGetDeviceProperties(&p, ordinal) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0;
 }
 
 int init_device(Device &d, int id) {
@@ -320,13 +320,27 @@ int init_device(Device &d, int id) {
     return CRC32C_OK;
 }
 
-int ensure_devices() {  // (call with g_dev_mu held)
-    if (g_ndev < 0) {
-        g_ndev = std::min(count_gfx950(), kMaxDevices);
-        for (int i = 0; i < g_ndev; ++i) g_devs.emplace_back(new Device());
-        g_ndev_pub.store(g_ndev, std::memory_order_release);
+int ensure_devices() {  // (call with g_dev_mu held): the number of gfx950 devices
+    if (g_nhip < 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) {
+            (void)hipGetLastError();
+            n = 0;
+        }
+        g_nhip = std::min(n, kMaxDevices);
+        for (int i = 0; i < g_nhip; ++i) {
+            g_devs.emplace_back(new Device());
+            if (is_gfx950(i)) g_gfx.push_back(i);
+        }
+        g_ngfx_pub.store((int)g_gfx.size(), std::memory_order_release);
     }
-    return g_ndev;
+    return (int)g_gfx.size();
+}
+
+int gfx_ordinal(int index) {  // library device index -> HIP ordinal (-1: none)
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    ensure_devices();
+    return index >= 0 && index < (int)g_gfx.size() ? g_gfx[index] : -1;
 }
 
 // Device state for the calling thread's current HIP device.  After a
@@ -342,7 +356,7 @@ int current_device(Device **out) {
     }
     std::lock_guard<std::mutex> lk(g_dev_mu);
     ensure_devices();
-    if (id < 0 || id >= g_ndev) return CRC32C_ENODEV;
+    if (id < 0 || id >= g_nhip) return CRC32C_ENODEV;
     Device &d = *g_devs[id];
     if (!d.ok) {
         const int rc = init_device(d, id);
@@ -1412,6 +1426,77 @@ int make_job(const crc32c_spans &s, unsigned flags, crc32c_job **out) {
     return CRC32C_OK;
 }
 
+// crc32c_batch_multi's workers: one persistent thread per gfx950 device,
+// bound to its HIP ordinal once (hipSetDevice) when first needed and kept for
+// the life of the process (detached; idle ones sleep on their condition
+// variable), so a call costs one hand-off per device rather than a thread
+// creation and a device bind (round 5 spawned a std::thread per device per
+// call).  Each worker runs its parts in the order they were posted; several
+// callers may use the pool at once.
+struct MultiDone {
+    std::mutex mu;
+    std::condition_variable cv;
+    int left = 0;
+    void add() {
+        std::lock_guard<std::mutex> lk(mu);
+        ++left;
+    }
+    void finish() {
+        std::lock_guard<std::mutex> lk(mu);
+        if (--left == 0) cv.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return left == 0; });
+    }
+};
+struct MultiJob {
+    crc32c_spans part;
+    int *rc;
+    MultiDone *done;
+};
+struct MultiWorker {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<MultiJob> q;
+    void post(const MultiJob &j) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            q.push_back(j);
+        }
+        cv.notify_one();
+    }
+    void run(int ordinal) {
+        const bool bound = hipSetDevice(ordinal) == hipSuccess;
+        for (;;) {
+            MultiJob j;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !q.empty(); });
+                j = q.front();
+                q.pop_front();
+            }
+            *j.rc = bound ? crc32c_batch(&j.part, 0, nullptr) : CRC32C_EHIP;
+            j.done->finish();
+        }
+    }
+};
+std::mutex g_multi_mu;
+MultiWorker *g_multi[kMaxDevices];
+
+MultiWorker *multi_worker(int index) {
+    if (index < 0 || index >= kMaxDevices) return nullptr;
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    if (!g_multi[index]) {
+        const int ordinal = gfx_ordinal(index);
+        if (ordinal < 0) return nullptr;
+        MultiWorker *w = new MultiWorker();  // (lives for the process)
+        std::thread([w, ordinal] { w->run(ordinal); }).detach();
+        g_multi[index] = w;
+    }
+    return g_multi[index];
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1420,7 +1505,7 @@ int make_job(const crc32c_spans &s, unsigned flags, crc32c_job **out) {
 extern "C" {
 
 int crc32c_gpu_count(void) {
-    const int n = g_ndev_pub.load(std::memory_order_acquire);
+    const int n = g_ngfx_pub.load(std::memory_order_acquire);
     if (n >= 0) return n;
     std::lock_guard<std::mutex> lk(g_dev_mu);
     return ensure_devices();
@@ -1730,29 +1815,29 @@ int crc32c_batch_multi(const crc32c_spans *s, int ngpus) {
     int rc = crc32c_shard_cuts(s->lens, s->len, s->n, ngpus, cut.data());
     if (rc) return rc;
     std::vector<int> rcs(ngpus, CRC32C_OK);
-    std::vector<std::thread> th;
+    MultiDone done;
     for (int g = 0; g < ngpus; ++g) {
-        th.emplace_back([&, g]() {
-            if (hipSetDevice(g) != hipSuccess) {
-                rcs[g] = CRC32C_EHIP;
-                return;
-            }
-            crc32c_spans sub = *s;
-            const uint64_t a0 = cut[g], a1 = cut[g + 1];
-            sub.n = a1 - a0;
-            if (sub.n == 0) return;
-            if (s->offsets) sub.offsets = s->offsets + a0;
-            else {
-                sub.base = (const uint8_t *)s->base + a0 * s->stride;
-                sub.base_bytes = s->base_bytes - a0 * s->stride;
-            }
-            if (s->lens) sub.lens = s->lens + a0;
-            if (s->crc_in) sub.crc_in = s->crc_in + a0;
-            sub.out = s->out + a0;
-            rcs[g] = crc32c_batch(&sub, 0, nullptr);
-        });
+        const uint64_t a0 = cut[g], a1 = cut[g + 1];
+        if (a1 == a0) continue;
+        crc32c_spans sub = *s;
+        sub.n = a1 - a0;
+        if (s->offsets) sub.offsets = s->offsets + a0;
+        else {
+            sub.base = (const uint8_t *)s->base + a0 * s->stride;
+            sub.base_bytes = s->base_bytes - a0 * s->stride;
+        }
+        if (s->lens) sub.lens = s->lens + a0;
+        if (s->crc_in) sub.crc_in = s->crc_in + a0;
+        sub.out = s->out + a0;
+        MultiWorker *w = multi_worker(g);
+        if (!w) {
+            rcs[g] = CRC32C_ENODEV;
+            continue;
+        }
+        done.add();
+        w->post(MultiJob{sub, &rcs[g], &done});
     }
-    for (auto &t : th) t.join();
+    done.wait();
     for (int r : rcs)
         if (r) return r;
     return CRC32C_OK;

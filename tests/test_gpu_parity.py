@@ -605,6 +605,83 @@ def test_config3_full_size(torch, span_path):
     bench._KEEP.clear()
 
 
+def test_planned_rounds_past_16_gib(torch, span_path):
+    """The balanced plan's rounds (crc32c_shim.hip plan_rounds: one per 8 GiB
+    of the batch's buffer, k_spans restarting every group's pipeline per
+    round) on a 17 GiB device buffer: 3 rounds, each cutting its third of the
+    plan's blocks (span order) into one share per span-kernel group.  Spans
+    sorted by offset over the whole buffer, some straddling the 8 and 16 GiB
+    marks, several MiB long ones among them: MODE 0 CRCs with and without
+    crc_in against the oracle.  Then 1 MiB wbufs of item images placed on
+    both sides of those marks and elsewhere: the device stamp (MODE 2) equals
+    the oracle's, the stamped images verify clean (MODE 1), and damaged ones
+    are reported exactly."""
+    if span_path == "small":
+        pytest.skip("a planned batch (the small path has no rounds)")
+    GiB, MiB = 1 << 30, 1 << 20
+    size = 17 * GiB
+    if torch.cuda.mem_get_info()[0] < size + 8 * GiB:
+        pytest.skip("needs about 25 GiB of free device memory")
+    rng = np.random.default_rng(1717)
+    data = torch.empty(size, dtype=torch.uint8, device="cuda")
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(17)
+    for c in range(0, size, GiB):
+        data[c:c + GiB] = torch.randint(0, 256, (GiB,), dtype=torch.uint8, device="cuda", generator=gen)
+    # spans: log-uniform 1 B - 1 MiB over the buffer, 100 across each mark, 12 of 2-6 MiB
+    n = 6000
+    lens = np.exp(rng.uniform(0, np.log(MiB), n)).astype(np.uint64)
+    lens[:12] = rng.integers(2 * MiB, 6 * MiB, 12)
+    offs = rng.integers(0, size - 8 * MiB, n).astype(np.uint64)
+    for k, mark in enumerate((8 * GiB, 16 * GiB)):
+        ix = np.arange(100 + 100 * k, 200 + 100 * k)
+        lens[ix] = np.maximum(lens[ix], 4096)
+        offs[ix] = mark - 1 - rng.integers(0, 2 ** 40, ix.size).astype(np.uint64) % (lens[ix] - 1)
+    order = np.argsort(offs, kind="stable")
+    offs, lens = offs[order], lens[order]
+    assert ((offs < 8 * GiB) & (offs + lens > 8 * GiB)).sum() >= 90
+    assert ((offs < 16 * GiB) & (offs + lens > 16 * GiB)).sum() >= 90
+    # the oracle over the spans' bytes, gathered on the device and copied once
+    cat = torch.cat([data[int(o):int(o + l)] for o, l in zip(offs, lens)]).cpu().numpy()
+    coffs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    cin = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    d_offs, d_lens = _dev(torch, offs.view(np.int64)), _dev(torch, lens.astype(np.uint32).view(np.int32))
+    for c in (None, cin):
+        got = mc.batch(data, offsets=d_offs, lens=d_lens, crc_in=None if c is None else _dev(torch, c.view(np.int32)))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(_u32(got), oracle.batch(cat, coffs, lens, c))
+    del cat
+    # item images: 1 MiB wbufs at MiB-aligned places around both marks and spread over the buffer
+    items = [layout.make_item(b"rd%06d" % i, rng.integers(0, 256, int(np.exp(rng.uniform(np.log(10), np.log(300000)))),
+                                                          dtype=np.uint8).tobytes(), cas=i + 1) for i in range(2500)]
+    hb, loc = layout.pack_wbufs(items, MiB)
+    nw = hb.size // MiB
+    near = [8 * GiB + (j - 12) * MiB for j in range(24)] + [16 * GiB + (j - 12) * MiB for j in range(24)]
+    spread = sorted(set(int(x) * MiB for x in rng.integers(0, size // MiB - 1, 4 * nw)) - set(near))
+    pos = np.asarray((near + spread[:max(0, nw - len(near))])[:nw], np.uint64)
+    assert pos.size == nw
+    for j in range(nw):
+        data[int(pos[j]):int(pos[j]) + MiB] = torch.from_numpy(hb[j * MiB:(j + 1) * MiB]).cuda()
+    ioffs = pos[(loc // MiB).astype(np.int64)] + loc % MiB
+    want = hb.copy()
+    so, sl = layout.spans_of(hb, loc)
+    layout.store_crcs(want, loc, oracle.batch(hb, so, sl))
+    d_ioffs = _dev(torch, ioffs.view(np.int64))
+    ok, nbad = mc.stamp_items(data, d_ioffs, region_bytes=MiB)
+    assert nbad == 0 and ok.cpu().numpy().all()
+    back = torch.cat([data[int(p):int(p) + MiB] for p in pos]).cpu().numpy()
+    np.testing.assert_array_equal(back, want)
+    ok, nbad = mc.verify_items(data, d_ioffs, region_bytes=MiB)
+    assert nbad == 0 and ok.cpu().numpy().all()
+    victims = sorted({int(np.argmax(ioffs > 8 * GiB)), int(np.argmax(ioffs > 16 * GiB)) - 1, loc.size - 1})
+    for v in victims:
+        o = int(ioffs[v])
+        data[o + 60] ^= 0x04
+    ok, nbad = mc.verify_items(data, d_ioffs, region_bytes=MiB)
+    assert nbad == len(victims) and np.flatnonzero(ok.cpu().numpy() == 0).tolist() == victims
+    del data
+
+
 @pytest.mark.parametrize("wbuf", [61, 64, 100, 127, 4099])
 def test_verify_pages_tiny_wbufs(torch, wbuf):
     """wbufs barely larger than one image (one item each, 48-B tail rule at

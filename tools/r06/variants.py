@@ -1,0 +1,70 @@
+"""Build A/B variants of libmcrc32c.so from edited copies of the sources
+(ab/NAME/src -> ab/NAME/libmcrc32c.so), so that the product sources carry no
+build switch.  Each variant is a list of (file, old, new) text edits; a
+missing `old` text fails the build.
+
+    python tools/r06/variants.py NAME [NAME ...]      # cur, lnst, lnc
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# The in-kernel stamp (round-6 review item 3): k_lines<2>'s epoch lane stores
+# the CRC into exptime at the end of its run (and ok = 1), no k_fix pass.
+_LN_FINISH_OLD = """                io.rt[item] = fused ? make_uint2(v, pad | kRtFused) : make_uint2(0u, 0u);
+                if (!sane) {"""
+_LN_FINISH_NEW = """                if (fused) {
+                    const uint32_t crc = ~mulmodp_dev(v, a.xpow[kXpowInv + pad]);
+                    uint8_t *q = const_cast<uint8_t *>(a.base) + p_pho + p_kh - 4;  // exptime (off + 28)
+                    STAMP_STORE
+                    if (a.ok) a.ok[item] = 1;
+                }
+                if (!sane) {"""
+_LN_SHIM_OLD = "    if (MODE == 2) {\n        // k_fix (the stamps"
+_LN_SHIM_NEW = "    if (MODE == 2 && false) {\n        // k_fix (the stamps"
+_NT = ("for (int b = 0; b < 4; ++b) __builtin_nontemporal_store((uint8_t)(crc >> (8 * b)), q + b);")
+_PLAIN = "for (int b = 0; b < 4; ++b) q[b] = (uint8_t)(crc >> (8 * b));"
+
+VARIANTS = {
+    "cur": [],
+    # byte-wise non-temporal stores, as k_fix's
+    "lnst": [("crc32c_kernels.hip", _LN_FINISH_OLD, _LN_FINISH_NEW.replace("STAMP_STORE", _NT)),
+             ("crc32c_shim.hip", _LN_SHIM_OLD, _LN_SHIM_NEW)],
+    # byte-wise default-policy stores
+    "lnc": [("crc32c_kernels.hip", _LN_FINISH_OLD, _LN_FINISH_NEW.replace("STAMP_STORE", _PLAIN)),
+            ("crc32c_shim.hip", _LN_SHIM_OLD, _LN_SHIM_NEW)],
+}
+
+
+def build(name):
+    out = os.path.join(ROOT, "ab", name)
+    src = os.path.join(out, "src")
+    shutil.rmtree(out, ignore_errors=True)
+    shutil.copytree(os.path.join(ROOT, "memcached_amd", "csrc"), os.path.join(src, "memcached_amd", "csrc"),
+                    ignore=shutil.ignore_patterns("_obj"))
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(src, "include"))
+    csrc = os.path.join(src, "memcached_amd", "csrc")
+    for f, old, new in VARIANTS[name]:
+        p = os.path.join(csrc, f)
+        text = open(p).read()
+        if old not in text:
+            raise SystemExit(f"{name}: edit target not found in {f}")
+        open(p, "w").write(text.replace(old, new, 1))
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-c", os.path.join(csrc, "crc32c_host.cpp"), "-o",
+                    os.path.join(out, "host.o")], check=True)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
+                    os.path.join(csrc, "crc32c_shim.hip"), "-o", os.path.join(out, "shim.o")], check=True)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
+                    os.path.join(out, "libmcrc32c.so"), os.path.join(out, "shim.o"), os.path.join(out, "host.o"),
+                    "-lpthread"], check=True)
+    for o in ("host.o", "shim.o"):
+        os.remove(os.path.join(out, o))
+    print(f"built ab/{name}/libmcrc32c.so")
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:]:
+        build(n)
