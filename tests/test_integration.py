@@ -172,3 +172,60 @@ def test_extstore_sim_without_fence_sees_false_badcrc(extstore_exe):
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert int(_fields(r.stdout.replace(",", ""))["badcrc"]) > 0
+
+
+# The reference's own extstore.c with the INTEGRATION.md section 2 hunks
+# (tests/integration/extstore_ref.patch), built in the build container by
+# oracle/build_extstore_ref.sh into oracle/_ref/ (test infrastructure, like
+# the reference crc32c.c build there); the binaries travel to the GPU box.
+_EXT_REF = os.path.join(ROOT, "oracle", "_ref", "extstore_ref")
+
+
+def _run_ext_ref(tmp_path, nofence=False, gpu=False):
+    exe = _EXT_REF + ("_nofence" if nofence else "")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/extstore_ref not built (no /root/reference where the tree was built)")
+    r = subprocess.run([exe, str(tmp_path), "8"], capture_output=True, text=True, timeout=300,
+                       env=None if gpu else _NOGPU)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("extstore_ref:")][0]
+    toks = line.split(":", 1)[1].split()
+    return {k: int(v) for k, v in zip(toks[0::2], toks[1::2])}
+
+
+def test_reference_extstore_deferred_stamp_with_fence_cpu(tmp_path):
+    """The reference extstore.c with the batched stamp at _submit_wbuf and the
+    open-wbuf fence, no GPU (the stamp hook falls back to storage.c:567 per
+    item): every read verifies, and reads of the open wbuf were stamped on
+    demand."""
+    f = _run_ext_ref(tmp_path)
+    assert f["badcrc"] == 0 and f["corrupt"] == 0 and f["short"] == 0
+    assert f["open_wbuf_stamps"] > 0 and f["fallback_batches"] > 0 and f["batches"] == 0
+    assert f["reads"] > 24000
+
+
+def test_reference_extstore_without_fence_sees_false_badcrc_cpu(tmp_path):
+    """Negative control: the fence hunk compiled out, reads of the open wbuf
+    see unstamped images (bad CRC, bytes intact)."""
+    f = _run_ext_ref(tmp_path, nofence=True)
+    assert f["badcrc"] > 0 and f["false_bad"] == f["badcrc"] and f["corrupt"] == 0
+
+
+@pytest.mark.gpu
+def test_reference_extstore_batched_stamp_gpu(tmp_path):
+    """The same run with the GPU: every submitted wbuf stamped by one
+    crc32c_stamp_items call inside the reference's _submit_wbuf, badcrc 0, and
+    the page file the reference's flush thread wrote verifies clean on the
+    device walk (crc32c_verify_pages)."""
+    f = _run_ext_ref(tmp_path, gpu=True)
+    assert f["badcrc"] == 0 and f["corrupt"] == 0 and f["short"] == 0 and f["open_wbuf_stamps"] > 0
+    assert f["batches"] > 0 and f["fallback_batches"] == 0 and f["stamp_nbad"] == 0
+    assert f["page_verify_rc"] == 0 and f["nbad"] == 0 and f["nitems"] >= 0.9 * f["written"]
+
+
+@pytest.mark.gpu
+def test_reference_extstore_without_fence_sees_false_badcrc_gpu(tmp_path):
+    f = _run_ext_ref(tmp_path, nofence=True, gpu=True)
+    assert f["batches"] > 0 and f["badcrc"] > 0 and f["false_bad"] == f["badcrc"] and f["corrupt"] == 0
+    assert f["page_verify_rc"] == 0 and f["nbad"] == 0
