@@ -458,8 +458,8 @@ def main(argv=None):
     ap.add_argument("--fill", default="splitmix", choices=["splitmix", "randint"],
                     help="item bytes: splitmix64(42 + rank) words (SURVEY.md 8d) or torch.randint")
     ap.add_argument("--workload", default="config2",
-                    choices=["config2", "config2r", "config3", "config5", "pagesmix", "mixed41", "pages", "stamp", "host",
-                             "calls", "multi"],
+                    choices=["config2", "config2r", "config3", "config5", "pagesmix", "mixed41", "pages", "pagesmixwalk",
+                             "stamp", "host", "calls", "multi"],
                     help="config2 = headline; others are extra measurements (not the bench line)")
     ap.add_argument("--pages", type=int, default=1000, help="config5: 64 MiB pages per GPU")
     ap.add_argument("--span-len", type=int, default=4133, help="config2r: span length (stride = len + 32)")
@@ -723,8 +723,11 @@ def extra_workload(args):
                                        "(K5 k_lines: 31-32 whole 128-B lines per span in one 4 KiB window, head and tail by the span's run lane)"},
                    kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
                    hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
-    elif args.workload in ("pages", "stamp"):
-        vargs, ok, victims, nbytes, cfg = workload_config5(args, rank, world)
+    elif args.workload in ("pages", "pagesmixwalk", "stamp"):
+        # pagesmixwalk: the mixed pages (workload_pagesmix) walked and verified on the device
+        walk = args.workload != "stamp"
+        vargs, ok, victims, nbytes, cfg = (workload_pagesmix if args.workload == "pagesmixwalk" else
+                                           workload_config5)(args, rank, world)
         base, size, region, offs, n, okp = vargs
         nitems, nbad = ctypes.c_uint64(0), ctypes.c_uint64(0)
         sptr = ctypes.c_void_p(stream.cuda_stream)
@@ -734,7 +737,7 @@ def extra_workload(args):
         wok = torch.empty(cap, dtype=torch.uint8, device="cuda")
 
         def one():
-            if args.workload == "pages":  # device walk + verify (storage.c:950-1070)
+            if walk:  # device walk + verify (storage.c:950-1070)
                 _lib.check(_lib.lib.crc32c_verify_pages(base, size, region, woffs.data_ptr(), wok.data_ptr(), cap,
                                                         ctypes.byref(nitems), ctypes.byref(nbad),
                                                         _lib.CRC32C_DEVICE, sptr))
@@ -755,11 +758,11 @@ def extra_workload(args):
         torch.cuda.synchronize()
         elapsed, evs = timed(steps, args.steps, world)
         kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
-        cfg["workload"] += (" -- walked on the device (crc32c_verify_pages)" if args.workload == "pages"
+        cfg["workload"] += (" -- walked on the device (crc32c_verify_pages)" if walk
                             else " -- stamped (crc32c_stamp_items)")
         res.update(config=cfg, kernel_ms=round(kms, 4), gib_s=round(nbytes * args.steps * world / elapsed / 2**30, 2),
                    hbm_frac=round(nbytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), nbad=int(nbad.value),
-                   nitems=int(nitems.value) if args.workload == "pages" else n, items_written=n)
+                   nitems=int(nitems.value) if walk else n, items_written=n)
     elif args.workload == "calls":
         # Per-call latency of the integration's call shapes (INTEGRATION.md
         # 2-4): wall clock of synchronous calls, launch and sync included.

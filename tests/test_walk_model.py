@@ -33,25 +33,30 @@ def seq_walk(buf, start, size):
     return out
 
 
-def wave_walk(buf, start, size):
-    """k_walk's loop, lane by lane (returns the offsets and the round trips)."""
+def wave_walk(buf, start, size, G=1):
+    """k_walk's loop, lane by lane (returns the offsets and the round trips).
+    G: guesses per lane per round trip (candidate q * 64 + j in lane j; the
+    width is 64 G).  The kernel reads one (G = 1); four were measured in round
+    6 and rejected (profiles/r06_ablations/walk_guesses_ab.txt), and the
+    walk's algebra holds for any G."""
+    W = WAVE * G
     out, off, s, trips = [], 0, 0, 0
     while off + 48 <= size:
         trips += 1
         lanes = []
-        for j in range(WAVE):
+        for j in range(W):
             o = off + j * s
             inb = (j == 0 or s != 0) and o + 48 <= size
             nkey = int(buf[start + o + 41]) if inb else 0
             nt = ntotal(buf, start + o) if inb else 48 + 1  # (header of zeros)
             item = inb and nkey != 0
             lanes.append((o, item, nt))
-        m = next((j for j, (_o, item, nt) in enumerate(lanes) if not (item and nt == s)), WAVE)
-        last_item = m < WAVE and lanes[m][1]
-        k = m + (1 if last_item else 0) if m < WAVE else WAVE
+        m = next((j for j, (_o, item, nt) in enumerate(lanes) if not (item and nt == s)), W)
+        last_item = m < W and lanes[m][1]
+        k = m + (1 if last_item else 0) if m < W else W
         out += [lanes[j][0] for j in range(k)]
-        if m == WAVE:
-            off += WAVE * s
+        if m == W:
+            off += W * s
         elif not last_item:
             break
         else:
@@ -70,11 +75,13 @@ def _pages(rng, sizes, wbuf, cut=0):
 def _check(buf, wbuf):
     for start in range(0, buf.size, wbuf):
         size = min(wbuf, buf.size - start)
-        got, _ = wave_walk(buf, start, size)
-        assert got == seq_walk(buf, start, size)
+        want = seq_walk(buf, start, size)
+        for G in (1, 4):  # (the kernel's one guess per lane, and four)
+            got, _ = wave_walk(buf, start, size, G)
+            assert got == want
 
 
-@pytest.mark.parametrize("run", [1, 2, 63, 64, 65, 127, 128, 129, 300])
+@pytest.mark.parametrize("run", [1, 2, 63, 64, 65, 127, 128, 129, 255, 256, 257, 300])
 def test_equal_runs(run):
     rng = np.random.default_rng(run)
     sizes = []
@@ -102,12 +109,15 @@ def test_corrupt_headers():
 
 
 def test_round_trips():
-    """Equal-sized items cost one round trip per 64 (plus the first)."""
+    """Equal-sized items cost one round trip per 64 G (plus the first): 17
+    for a 1007-item wbuf at the kernel's G = 1."""
     rng = np.random.default_rng(3)
     wbuf = 4 << 20
     buf = _pages(rng, [4096] * 1007, wbuf)
-    got, trips = wave_walk(buf, 0, wbuf)
-    assert len(got) == 1007 and trips == 1 + -(-1006 // WAVE) + (1 if 1006 % WAVE == 0 else 0)
+    for G in (1, 4):
+        got, trips = wave_walk(buf, 0, wbuf, G)
+        W = WAVE * G
+        assert len(got) == 1007 and trips == 1 + -(-1006 // W) + (1 if 1006 % W == 0 else 0)
 
 
 @pytest.mark.parametrize("wbuf", [48, 49, 61, 64, 100, 127])

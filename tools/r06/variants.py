@@ -3,7 +3,7 @@
 build switch.  Each variant is a list of (file, old, new) text edits; a
 missing `old` text fails the build.
 
-    python tools/r06/variants.py NAME [NAME ...]      # cur, lnst, lnc
+    python tools/r06/variants.py NAME [NAME ...]      # cur, lnst, lnc, git:REV
 """
 import os
 import shutil
@@ -40,14 +40,21 @@ VARIANTS = {
 
 
 def build(name):
-    out = os.path.join(ROOT, "ab", name)
+    """NAME from VARIANTS, or git:REV -- the sources of commit REV (built into ab/REV)."""
+    rev = name[4:] if name.startswith("git:") else None
+    out = os.path.join(ROOT, "ab", rev or name)
     src = os.path.join(out, "src")
     shutil.rmtree(out, ignore_errors=True)
     shutil.copytree(os.path.join(ROOT, "memcached_amd", "csrc"), os.path.join(src, "memcached_amd", "csrc"),
                     ignore=shutil.ignore_patterns("_obj"))
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(src, "include"))
     csrc = os.path.join(src, "memcached_amd", "csrc")
-    for f, old, new in VARIANTS[name]:
+    if rev:
+        for d, files in (("memcached_amd/csrc", os.listdir(csrc)), ("include", os.listdir(os.path.join(src, "include")))):
+            for f in files:
+                text = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:{d}/{f}"], check=True, capture_output=True).stdout
+                open(os.path.join(src, d, f), "wb").write(text)
+    for f, old, new in ([] if rev else VARIANTS[name]):
         p = os.path.join(csrc, f)
         text = open(p).read()
         if old not in text:
@@ -62,7 +69,7 @@ def build(name):
                     "-lpthread"], check=True)
     for o in ("host.o", "shim.o"):
         os.remove(os.path.join(out, o))
-    print(f"built ab/{name}/libmcrc32c.so")
+    print(f"built ab/{rev or name}/libmcrc32c.so")
 
 
 if __name__ == "__main__":
