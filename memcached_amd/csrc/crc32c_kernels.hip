@@ -2449,7 +2449,9 @@ __global__ void k_chain(const uint32_t *iov_crc, const uint32_t *lens, uint32_t 
 // it ends the wbuf (nkey == 0, or fewer than 48 bytes left), and the walk goes
 // on from lane m's item end with s = its ntotal.  Whatever the data, the
 // result is the sequential walk's (tests/test_walk_model.py restates it);
-// equal-sized items cost one round trip per 64 of them.
+// equal-sized items cost one round trip per 64 of them.  Round 6: after a
+// round trip whose guesses broke at lane 0 or 1 the next one guesses once
+// (lane 0 alone reads a header), and widens again when that guess holds.
 constexpr uint32_t kWalkWaves = 4;  // waves (wbufs) per workgroup
 
 struct WalkOut {
@@ -2494,26 +2496,33 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
         }
         uint64_t off = 0, s = 0;  // wave-uniform: next item, stride guess (0: none yet)
         uint32_t c = 0;           // items walked so far
+        // guesses this round trip: 64, or 1 after a round trip whose guesses
+        // broke at once (round 6: a wbuf of mixed sizes breaks every guess at
+        // its first lane, and 63 wasted header reads per item flooded HBM --
+        // 19 us per round trip on the mixed pages; one read per item until a
+        // size repeats)
+        uint32_t wid = 1;
         while (off + 48 <= size) {
             const uint64_t o = off + j * s;
-            const bool in = (j == 0 || s != 0) && o + 48 <= size;  // (s < 2^33: no overflow)
+            const bool in = j < wid && (j == 0 || s != 0) && o + 48 <= size;  // (s < 2^33: no overflow)
             ItemHdr h{0u, 0u, 0u, 0u};
             if (in) h = parse_hdr(wb + o);
             const uint64_t nt = h.ntotal(a.cfl);
             const bool item = in && h.nkey != 0;
-            // m = the first lane whose successor's guess is wrong (64: none)
-            const uint64_t brk = __ballot(!(item && nt == s));
-            const uint32_t m = brk ? (uint32_t)__ffsll((unsigned long long)brk) - 1u : 64u;
+            // m = the first lane whose successor's guess is wrong (wid: none;
+            // lanes past wid guessed nothing)
+            const uint64_t brk = __ballot(!(item && nt == s)) & (wid >= 64u ? ~0ull : (1ull << wid) - 1ull);
+            const uint32_t m = brk ? (uint32_t)__ffsll((unsigned long long)brk) - 1u : wid;
             // lane m (if any) is on a true boundary: an item, or the end of the
             // wbuf.  Its flag and size are broadcast to every lane (ds_bpermute),
             // and the walk state stays in VGPRs, equal in all lanes: with it in
-            // SGPRs from readlane the walk went wrong on large page sets (the
-            // same ISA read correct by hand)
-            const int src = m < 64u ? (int)m : 0;
-            const bool last_item = m < 64u && __shfl((int)item, src, 64) != 0;
+            // SGPRs from readlane the walk went wrong on large page sets (round
+            // 2)
+            const int src = m < wid ? (int)m : 0;
+            const bool last_item = m < wid && __shfl((int)item, src, 64) != 0;
             const uint64_t nt_m = (uint64_t)(uint32_t)__shfl((int)(uint32_t)nt, src, 64) |
                                   ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(nt >> 32), src, 64) << 32);
-            const uint32_t k = m < 64u ? m + (last_item ? 1u : 0u) : 64u;  // items this round trip
+            const uint32_t k = m < wid ? m + (last_item ? 1u : 0u) : wid;  // items this round trip
             if (!EMIT && out.slots && j < k && c + j < out.kslot) out.slots[w * out.kslot + c + j] = start + o;
             if (EMIT && j < k && c + j < expect) {
                 const uint64_t i = first + c + j;
@@ -2521,13 +2530,15 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
                 if (plan) count_item<1>(a, i, item_desc(a, start + o, h, true), t8, out.nunit, out.irec, out.fast);
             }
             c += k;
-            if (m == 64u) {
-                off += 64u * s;
+            if (m == wid) {
+                off += wid * s;  // every guess right: the size repeats
+                wid = 64u;
             } else if (!last_item) {
                 break;  // lane m ends the wbuf
             } else {
                 off += m * s + nt_m;
                 s = nt_m;
+                wid = m <= 1u ? 1u : 64u;
             }
         }
         if (!EMIT && j == 0) out.cnt[w] = c;

@@ -33,14 +33,17 @@ def seq_walk(buf, start, size):
     return out
 
 
-def wave_walk(buf, start, size, G=1):
+def wave_walk(buf, start, size, G=1, adaptive=True):
     """k_walk's loop, lane by lane (returns the offsets and the round trips).
     G: guesses per lane per round trip (candidate q * 64 + j in lane j; the
     width is 64 G).  The kernel reads one (G = 1); four were measured in round
     6 and rejected (profiles/r06_ablations/walk_guesses_ab.txt), and the
-    walk's algebra holds for any G."""
-    W = WAVE * G
+    walk's algebra holds for any G.  adaptive (the kernel since round 6):
+    after a round trip whose guesses broke at lane 0 or 1, the next one
+    guesses with lane 0 alone, and widens again when that guess holds."""
+    full = WAVE * G
     out, off, s, trips = [], 0, 0, 0
+    W = 1 if adaptive else full
     while off + 48 <= size:
         trips += 1
         lanes = []
@@ -57,11 +60,13 @@ def wave_walk(buf, start, size, G=1):
         out += [lanes[j][0] for j in range(k)]
         if m == W:
             off += W * s
+            W = full
         elif not last_item:
             break
         else:
             off += m * s + lanes[m][2]
             s = lanes[m][2]
+            W = 1 if (adaptive and m <= 1) else full
     return out, trips
 
 
@@ -77,8 +82,9 @@ def _check(buf, wbuf):
         size = min(wbuf, buf.size - start)
         want = seq_walk(buf, start, size)
         for G in (1, 4):  # (the kernel's one guess per lane, and four)
-            got, _ = wave_walk(buf, start, size, G)
-            assert got == want
+            for adaptive in (True, False):  # (the kernel since round 6, and before)
+                got, _ = wave_walk(buf, start, size, G, adaptive)
+                assert got == want
 
 
 @pytest.mark.parametrize("run", [1, 2, 63, 64, 65, 127, 128, 129, 255, 256, 257, 300])
@@ -109,15 +115,21 @@ def test_corrupt_headers():
 
 
 def test_round_trips():
-    """Equal-sized items cost one round trip per 64 G (plus the first): 17
-    for a 1007-item wbuf at the kernel's G = 1."""
+    """Equal-sized items cost one round trip per 64 (plus two to learn the
+    size: one guess after the first item, then 64 per trip); items of mixed
+    sizes one round trip each, with one header read per trip."""
     rng = np.random.default_rng(3)
     wbuf = 4 << 20
     buf = _pages(rng, [4096] * 1007, wbuf)
-    for G in (1, 4):
-        got, trips = wave_walk(buf, 0, wbuf, G)
-        W = WAVE * G
-        assert len(got) == 1007 and trips == 1 + -(-1006 // W) + (1 if 1006 % W == 0 else 0)
+    got, trips = wave_walk(buf, 0, wbuf)
+    assert len(got) == 1007 and trips == 2 + -(-1005 // WAVE) + (1 if 1005 % WAVE == 0 else 0)
+    got, trips = wave_walk(buf, 0, wbuf, adaptive=False)
+    assert len(got) == 1007 and trips == 1 + -(-1006 // WAVE) + (1 if 1006 % WAVE == 0 else 0)
+    sizes = [int(x) for x in np.exp(rng.uniform(np.log(512), np.log(65536), 300))]
+    buf = _pages(rng, sizes, wbuf)
+    want = seq_walk(buf, 0, wbuf)
+    got, trips = wave_walk(buf, 0, wbuf)
+    assert got == want and trips <= len(want) + 1
 
 
 @pytest.mark.parametrize("wbuf", [48, 49, 61, 64, 100, 127])
