@@ -28,8 +28,15 @@ _LN_SHIM_NEW = "    if (MODE == 2 && false) {\n        // k_fix (the stamps"
 _NT = ("for (int b = 0; b < 4; ++b) __builtin_nontemporal_store((uint8_t)(crc >> (8 * b)), q + b);")
 _PLAIN = "for (int b = 0; b < 4; ++b) q[b] = (uint8_t)(crc >> (8 * b));"
 
+# K5's runs dealt in chunks of 16 consecutive runs (about one 4 MiB wbuf of
+# 4165-B images) instead of one run at a time: the locality a K5 that walks
+# its own wbufs would have
+_RUN_OLD = "    auto run_start = [&](uint64_t k) -> uint64_t { return (k * W + w0) * run_imgs; };"
+_RUN_NEW = ("    auto run_start = [&](uint64_t k) -> uint64_t { return (((k >> 4) * W + w0) * 16 + (k & 15)) * run_imgs; };")
+
 VARIANTS = {
     "cur": [],
+    "chunk16": [("crc32c_kernels.hip", _RUN_OLD, _RUN_NEW)],
     # byte-wise non-temporal stores, as k_fix's
     "lnst": [("crc32c_kernels.hip", _LN_FINISH_OLD, _LN_FINISH_NEW.replace("STAMP_STORE", _NT)),
              ("crc32c_shim.hip", _LN_SHIM_OLD, _LN_SHIM_NEW)],
