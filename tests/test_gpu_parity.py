@@ -1149,7 +1149,8 @@ def test_python_device_descriptor_checks(torch):
 
 
 def test_verify_pages_count_only_query(torch):
-    """cap == 0 counts the walk's items and verifies nothing."""
+    """cap == 0 counts the walk's items and verifies nothing; a cap below the
+    count still verifies every item."""
     import ctypes
     rng = np.random.default_rng(43)
     items = [layout.make_item(b"q%05d" % i, rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes(),
@@ -1169,3 +1170,23 @@ def test_verify_pages_count_only_query(torch):
     # host path: capacity bound from the header
     got_offs, got_ok, nb = mc.verify_pages(buf, wbuf)
     assert nb == 1 and got_offs.size == offs.size
+    # a capacity below the item count: the first cap items and verdicts, the
+    # full count, every item verified (device and host arrays)
+    cap = offs.size // 2
+    want_ok = np.ones(cap, np.uint8)
+    want_ok[10] = 0
+    d_offs = _dev(torch, np.full(cap + 5, -1, np.int64))
+    d_ok = _dev(torch, np.full(cap + 5, 7, np.uint8))
+    _lib.check(_lib.lib.crc32c_verify_pages(d.data_ptr(), buf.size, wbuf, d_offs.data_ptr(), d_ok.data_ptr(), cap,
+                                            ctypes.byref(nitems), ctypes.byref(nbad), _lib.CRC32C_DEVICE, None))
+    torch.cuda.synchronize()
+    assert nitems.value == offs.size and nbad.value == 1
+    np.testing.assert_array_equal(d_offs.cpu().numpy()[:cap].astype(np.uint64), offs[:cap])
+    np.testing.assert_array_equal(d_ok.cpu().numpy()[:cap], want_ok)
+    assert (d_offs.cpu().numpy()[cap:] == -1).all() and (d_ok.cpu().numpy()[cap:] == 7).all()
+    h_offs, h_ok = np.zeros(cap, np.uint64), np.zeros(cap, np.uint8)
+    _lib.check(_lib.lib.crc32c_verify_pages(buf.ctypes.data, buf.size, wbuf, h_offs.ctypes.data, h_ok.ctypes.data, cap,
+                                            ctypes.byref(nitems), ctypes.byref(nbad), 0, None))
+    assert nitems.value == offs.size and nbad.value == 1
+    np.testing.assert_array_equal(h_offs, offs[:cap])
+    np.testing.assert_array_equal(h_ok, want_ok)
