@@ -34,8 +34,15 @@ _PLAIN = "for (int b = 0; b < 4; ++b) q[b] = (uint8_t)(crc >> (8 * b));"
 _RUN_OLD = "    auto run_start = [&](uint64_t k) -> uint64_t { return (k * W + w0) * run_imgs; };"
 _RUN_NEW = ("    auto run_start = [&](uint64_t k) -> uint64_t { return (((k >> 4) * W + w0) * 16 + (k & 15)) * run_imgs; };")
 
+# K1 with the table image's 32 replicas used as 16 (lanes l and l + 16 read
+# the same replica: the two-way bank conflicts of a half-replicated image, the
+# room an LDS-DMA K1 would stage into), same instructions otherwise
+_K1_LANE_OLD = "    c.lane4 = li << 2;\n    c.lane4hi = c.lane4 | 0x10000u;\n    const uint64_t waves = blockDim.x >> 6;"
+_K1_LANE_NEW = "    c.lane4 = (li & 15u) << 2;\n    c.lane4hi = c.lane4 | 0x10000u;\n    const uint64_t waves = blockDim.x >> 6;"
+
 VARIANTS = {
     "cur": [],
+    "k1half": [("crc32c_kernels.hip", _K1_LANE_OLD, _K1_LANE_NEW)],
     "chunk16": [("crc32c_kernels.hip", _RUN_OLD, _RUN_NEW)],
     # byte-wise non-temporal stores, as k_fix's
     "lnst": [("crc32c_kernels.hip", _LN_FINISH_OLD, _LN_FINISH_NEW.replace("STAMP_STORE", _NT)),
