@@ -1757,12 +1757,17 @@ int crc32c_verify_pages(const void *base, uint64_t base_bytes, uint64_t wbuf_byt
     a.offsets = doffs;
     a.ok = dok;
     a.n = total;
-    // the second walk writes the offsets and, for a planned verify, the plan
-    // entries k_count would make (the headers are read once more, not twice)
+    // The emit pass writes the offsets: copied from the count pass's slots,
+    // or for a wbuf of more items than those (or with no slots kept) by
+    // walking it again.  A planned verify then reads the headers in k_count,
+    // in parallel (round 6; the emit pass used to walk again and write
+    // k_count's entries itself, one header per round trip on mixed pages);
+    // only when no slots are kept does the second walk write the entries
+    // too (the headers are then read once more, not twice).
     Path path;
     path.small = takes_small<1>(a);
     const bool k5 = !path.small && items_fused(a);  // (then the walk writes offsets only)
-    path.counted = !path.small && !k5;
+    path.counted = !path.small && !k5 && wo.kslot == 0;
     if (path.counted) {
         rc = ensure_plan(*d, total, plan_cap(a));
         if (rc) return rc;
