@@ -2514,14 +2514,18 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(SpanArgs a, uint64_t n
             const uint64_t brk = __ballot(!(item && nt == s)) & (wid >= 64u ? ~0ull : (1ull << wid) - 1ull);
             const uint32_t m = brk ? (uint32_t)__ffsll((unsigned long long)brk) - 1u : wid;
             // lane m (if any) is on a true boundary: an item, or the end of the
-            // wbuf.  Its flag and size are broadcast to every lane (ds_bpermute),
-            // and the walk state stays in VGPRs, equal in all lanes: with it in
-            // SGPRs from readlane the walk went wrong on large page sets (round
-            // 2)
-            const int src = m < wid ? (int)m : 0;
-            const bool last_item = m < wid && __shfl((int)item, src, 64) != 0;
-            const uint64_t nt_m = (uint64_t)(uint32_t)__shfl((int)(uint32_t)nt, src, 64) |
-                                  ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(nt >> 32), src, 64) << 32);
+            // wbuf.  Its flag and size are read out of lane m into scalars
+            // (v_readlane: the walk state is scalar).  Round 6: the walk kept
+            // its state in VGPRs through round 5, broadcast with ds_bpermute,
+            // because readlane variants had gone wrong on large page sets in
+            // round 2 -- the 64-bit shift hazard of the header parse (DESIGN.md
+            // 3.6), since removed; the bpermutes' LDS round trips were most of
+            // a narrow round trip's time
+            const uint32_t src = m < wid ? m : 0u;
+            const bool last_item = m < wid && __builtin_amdgcn_readlane((int)item, (int)src) != 0;
+            const uint64_t nt_m = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)nt, (int)src) |
+                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(nt >> 32), (int)src)
+                                   << 32);
             const uint32_t k = m < wid ? m + (last_item ? 1u : 0u) : wid;  // items this round trip
             if (!EMIT && out.slots && j < k && c + j < out.kslot) out.slots[w * out.kslot + c + j] = start + o;
             if (EMIT && j < k && c + j < expect) {
