@@ -814,6 +814,19 @@ def extra_workload(args):
         verify64_pin_us = per_call(lambda: _lib.check(_lib.lib.crc32c_verify_items(
             wb_pin.data_ptr(), region, region, hoffs_w.ctypes.data, 64, hok.ctypes.data, ctypes.byref(nbad), 0,
             None)), 200)
+        # the compaction readback's shape (storage.c:950-1070, INTEGRATION.md
+        # 3): one wbuf walked and verified, device-resident and page-locked
+        nitems_w = ctypes.c_uint64(0)
+        wcap = per_wbuf + 1
+        d_woffs = torch.empty(wcap, dtype=torch.int64, device="cuda")
+        d_wok = torch.empty(wcap, dtype=torch.uint8, device="cuda")
+        h_woffs, h_wok = np.empty(wcap, np.uint64), np.empty(wcap, np.uint8)
+        pages_wbuf_us = per_call(lambda: _lib.check(_lib.lib.crc32c_verify_pages(
+            base, region, region, d_woffs.data_ptr(), d_wok.data_ptr(), wcap, ctypes.byref(nitems_w),
+            ctypes.byref(nbad), _lib.CRC32C_DEVICE, sptr)), 200)
+        pages_wbuf_pin_us = per_call(lambda: _lib.check(_lib.lib.crc32c_verify_pages(
+            wb_pin.data_ptr(), region, region, h_woffs.ctypes.data, h_wok.ctypes.data, wcap, ctypes.byref(nitems_w),
+            ctypes.byref(nbad), 0, None)), 100)
         pin64 = torch.from_numpy(host).pin_memory()
         hs_pin = _lib.Spans(pin64.data_ptr(), host.size, hoffs.ctypes.data, 0, None, 4133, None, hout.ctypes.data, 64)
         host64_pin_us = per_call(lambda: _lib.check(_lib.lib.crc32c_batch(ctypes.byref(hs_pin), 0, None)), 200)
@@ -855,12 +868,13 @@ def extra_workload(args):
                                        "1007 images (device; host page-locked; host pageable), verify an IO batch "
                                        "of 64 images (device; host page-locked), CRC 64 x 4133-B spans in host "
                                        "memory (pageable: staged; page-locked: the coalescing queue) and in device "
-                                       "memory"},
+                                       "memory, walk + verify one wbuf (device; host page-locked)"},
                    stamp_wbuf_us=round(stamp_us, 1), verify64_us=round(verify64_us, 1),
                    stamp_wbuf_host_pinned_us=round(stamp_pin_us, 1), stamp_wbuf_host_pageable_us=round(stamp_page_us, 1),
                    verify64_host_pinned_us=round(verify64_pin_us, 1),
                    host_batch64_us=round(host64_us, 1), host_batch64_pinned_us=round(host64_pin_us, 1),
                    device_batch64_us=round(dev64_us, 1),
+                   pages_wbuf_us=round(pages_wbuf_us, 1), pages_wbuf_host_pinned_us=round(pages_wbuf_pin_us, 1),
                    stamp_wbuf_gb_s=round(per_wbuf * 4133 / (stamp_us * 1e-6) / 1e9, 1),
                    stamp_wbuf_host_pinned_gb_s=round(per_wbuf * 4133 / (stamp_pin_us * 1e-6) / 1e9, 1))
     else:  # host: pinned host memory -> H2D -> K1/K2 -> D2H through the library's host path
