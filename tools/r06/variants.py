@@ -40,8 +40,66 @@ _RUN_NEW = ("    auto run_start = [&](uint64_t k) -> uint64_t { return (((k >> 4
 _K1_LANE_OLD = "    c.lane4 = li << 2;\n    c.lane4hi = c.lane4 | 0x10000u;\n    const uint64_t waves = blockDim.x >> 6;"
 _K1_LANE_NEW = "    c.lane4 = (li & 15u) << 2;\n    c.lane4hi = c.lane4 | 0x10000u;\n    const uint64_t waves = blockDim.x >> 6;"
 
+# load_block with one address per lane and the loads' immediate offsets when
+# every piece of every lane of the wave lies at or past its span's first
+# piece (every block but a unit's head block): no per-piece select
+_LB_OLD = """#pragma unroll
+    for (int j = 0; j < (int)kK1Pieces; ++j) {
+        const uint8_t *q = e0 + j * (int32_t)kK1Piece > 0 ? q0 + j * kK1Piece : zl;
+        w.v[j] = kSpanNT ? ld16_nt(q) : ld16(q);
+    }
+}"""
+_LB_NEW = """    if (__builtin_amdgcn_readfirstlane(__all(e0 > 0))) {
+#pragma unroll
+        for (int j = 0; j < (int)kK1Pieces; ++j) w.v[j] = kSpanNT ? ld16_nt(q0 + j * kK1Piece) : ld16(q0 + j * kK1Piece);
+    } else {
+#pragma unroll
+        for (int j = 0; j < (int)kK1Pieces; ++j) {
+            const uint8_t *q = e0 + j * (int32_t)kK1Piece > 0 ? q0 + j * kK1Piece : zl;
+            w.v[j] = kSpanNT ? ld16_nt(q) : ld16(q);
+        }
+    }
+}"""
+
+# k_spans<true>'s record cursor and share end in 32 bits (a plan holds fewer
+# than 2^32 records): two VGPRs fewer where the kernel spills
+_U32_OLD = """    uint64_t u = g;
+    uint64_t ub = nunits;  // the group's records (of this round) end here"""
+_U32_NEW = """    // (UNITS: a plan holds fewer than 2^32 records -- 32-bit cursors, two
+    // VGPRs fewer)
+    using Idx = typename std::conditional<UNITS, uint32_t, uint64_t>::type;
+    Idx u = g;
+    Idx ub = (Idx)nunits;  // the group's records (of this round) end here"""
+_U32S_OLD = "    const uint64_t ustep = bal ? 1u : ngroups_total;"
+_U32S_NEW = "    const Idx ustep = bal ? 1u : (Idx)ngroups_total;"
+
+# the lane index re-derived (v_mbcnt, volatile: not hoisted) where a unit
+# switch uses it, so that no lane constant is live across the block loop
+_RM_OLD = """        UnitDesc nd;
+        if (__any(last)) {
+            const uint32_t g = lane & 32u, sb = sl << 3;
+            const uint32_t rw = __shfl(ring, g | sb | (li & 7u), 64);  // slot sl, dword li & 7
+            nd = decode_unit<UNITS>(a, rw, u + ustep, nunits, lane);
+        }
+        if (last && (li >> 3) == sl) ring = fetch_unit<UNITS>(a, u + 5 * ustep, ub, li);"""
+_RM_NEW = r"""        UnitDesc nd;
+        uint32_t ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        const uint32_t lj = ln & 31u;
+        if (__any(last)) {
+            const uint32_t g = ln & 32u, sb = sl << 3;
+            const uint32_t rw = __shfl(ring, g | sb | (lj & 7u), 64);  // slot sl, dword li & 7
+            nd = decode_unit<UNITS>(a, rw, u + ustep, nunits, ln);
+        }
+        if (last && (lj >> 3) == sl) ring = fetch_unit<UNITS>(a, u + 5 * ustep, ub, lj);"""
+
 VARIANTS = {
     "cur": [],
+    "remat": [("crc32c_kernels.hip", _RM_OLD, _RM_NEW)],
+    "u32remat": [("crc32c_kernels.hip", _U32_OLD, _U32_NEW), ("crc32c_kernels.hip", _U32S_OLD, _U32S_NEW),
+                 ("crc32c_kernels.hip", _RM_OLD, _RM_NEW)],
+    "u32": [("crc32c_kernels.hip", _U32_OLD, _U32_NEW), ("crc32c_kernels.hip", _U32S_OLD, _U32S_NEW)],
+    "lbfast": [("crc32c_kernels.hip", _LB_OLD, _LB_NEW)],
     "k1half": [("crc32c_kernels.hip", _K1_LANE_OLD, _K1_LANE_NEW)],
     "chunk16": [("crc32c_kernels.hip", _RUN_OLD, _RUN_NEW)],
     # byte-wise non-temporal stores, as k_fix's
