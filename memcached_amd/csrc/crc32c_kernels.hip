@@ -1980,7 +1980,7 @@ struct ItemsOut {
     uint32_t *nfb;  // their count
     const uint32_t *route;  // k_census's verdict (nullptr: take the batch); 0: every image to the planned path
     uint2 *rt;      // MODE 2: per item {M_t(f), t | kRtFused}, {0, 0} if not fused (for k_fix)
-    const uint32_t *xk;  // k_lines: x^(8e) for e in [kXkLo, kXkLo + kXkN)
+    uint32_t xm128;      // k_lines: x^(-8 * 128) (MODE 0: the CRC from M_128(V))
     uint32_t nsr;        // k_lines: steps per run (a wave's run is 2 nsr consecutive images)
 };
 constexpr uint32_t kRtFused = 0x80000000u;
@@ -2042,15 +2042,19 @@ struct ItemBuf {
 //   - the group's R = raw of the window goes back to the image's epoch lane,
 //     which at the end of the run forms
 //       V = M_{Et-A}(r_h) ^ M_{Et-A-4096}(R) ^ r_t = M_pad(f),
-//     f the register after D from ~c, pad = Et - E (x^(8e) from the xk table,
-//     e in [-128, 4352)): crc32c(c, D) = ~M_{-pad}(V); a verify is good iff
-//     V == M_pad(~stored).
+//     f the register after D from ~c, pad = Et - E: crc32c(c, D) =
+//     ~M_{-pad}(V); a verify is good iff V == M_pad(~stored).  Round 6: the
+//     lane forms W = M_128(V) = M_d(M_4096(r_h) ^ R) ^ M_128(r_t), d = Et - A
+//     - 3968 in [0, 272), with the table operators (M_2048 twice, the tree
+//     levels M_16..M_128 by the bits of d, zeros_lds below 16) instead of two
+//     bitwise multiplies by x^(8 (Et - A)) and x^(8 (Et - A - 4096)) (the
+//     second negative for a 31-line window with a short tail, hence the
+//     M_128): a verify is good iff W == M_128(M_pad(~stored)), the CRC is
+//     ~M_{-pad-128}(W).
 // tests/test_items_lines_model.py restates it on the CPU.
 constexpr uint32_t kLineBytes = 128;
 constexpr uint32_t kHeadPieces = 10;  // 16-B pieces of [floor16(p), A): A - p <= 131
 constexpr uint32_t kTailPieces = 9;   // of [B, Et): Et - B < 128 + 16
-constexpr int32_t kXkLo = -128;
-constexpr uint32_t kXkN = 4480;       // e in [-128, 4352)
 constexpr uint32_t kSt31 = 0x80u;     // the window holds 31 lines (row 3, lanes 28-31: zeros)
 
 // The fused shape: B - A (bytes of whole lines inside the span after the
@@ -2111,8 +2115,8 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
         // branch leaves the waitcnt pass a merged state that waits for it)
         return valid_of(r) ? (OFFS ? a.offsets[item_of(r)] : item_of(r) * a.stride) : 0;
     };
-    // MODE 0: x^(-8t), t < 16, lane-distributed (lane j holds t = j & 15)
-    const uint32_t xinv = MODE == 0 ? a.xpow[kXpowInv + (lane & 15u)] : 0u;
+    // MODE 0: x^(-8 (t + 128)), t < 16, lane-distributed (lane j holds t = j & 15)
+    const uint32_t xinv = MODE == 0 ? mulmodp_dev(a.xpow[kXpowInv + (lane & 15u)], io.xm128) : 0u;
     uint64_t noff = off_of(0);  // this lane's image offset in the wave's next run
     uint32_t ncin = MODE == 0 && a.crc_in && valid_of(0) ? a.crc_in[item_of(0)] : 0u;
 
@@ -2237,10 +2241,16 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
         // (every lane: a lane-distributed value read under a branch would come
         // from lanes the branch left inactive)
         const uint32_t xt = MODE == 0 ? (uint32_t)__shfl((int)xinv, (int)pad, 64) : 0u;
-        uint32_t v = 0;
+        uint32_t v = 0;  // W = M_128(V) = M_{pad + 128}(f)
         if (fused) {
-            const uint32_t x1 = io.xk[p_eta - kXkLo], x2 = io.xk[p_eta - kBlockBytes - kXkLo];
-            v = mulmodp_dev(r_h, x1) ^ mulmodp_dev(er, x2) ^ r_t;  // M_pad(f)
+            const uint32_t dl = p_eta - (kBlockBytes - kLineBytes);  // d = Et - A - 3968
+            uint32_t y = apply_op<4>(kAuxSpanFold, apply_op<4>(kAuxSpanFold, r_h)) ^ er;
+            if (dl & 256u) y = apply_op<4>(kAuxTree + 12, apply_op<4>(kAuxTree + 12, y));
+            if (dl & 128u) y = apply_op<4>(kAuxTree + 12, y);
+            if (dl & 64u) y = apply_op<4>(kAuxTree + 8, y);
+            if (dl & 32u) y = apply_op<4>(kAuxTree + 4, y);
+            if (dl & 16u) y = apply_op<4>(kAuxTree, y);
+            v = zeros_lds(y, dl & 15u, c) ^ apply_op<4>(kAuxTree + 12, r_t);
         }
         if (valid) {
             if (MODE == 0) {
@@ -2248,7 +2258,7 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
                 nb += !sane;  // (out of the buffer: not read, out 0, counted)
             } else if (MODE == 1) {
                 if (fused || !sane) {
-                    const bool good = fused && v == zeros_lds(~p_stored, pad, c);
+                    const bool good = fused && v == apply_op<4>(kAuxTree + 12, zeros_lds(~p_stored, pad, c));
                     a.ok[item] = good;
                     nb += !good;
                 }
@@ -2333,20 +2343,21 @@ __global__ __launch_bounds__(1024) void k_lines(SpanArgs a, const uint4 *__restr
 }
 
 
-// The last step of a K5 stamp (MODE 2), one thread per image: from R = M_t(f),
-// f the register after the span from ~0, the CRC is ~M_{-t}(R), stamped into
+// The last step of a K5 stamp (MODE 2), one thread per image: from W =
+// M_{t + 128}(f), f the register after the span from ~0, the CRC is
+// ~M_{-t-128}(W) (xm128 = x^(-8 * 128)), stamped into
 // the image's exptime as the spill CRC (storage.c:567).  A separate pass:
 // within k_lines an image's stamp could race with another wave's read of the
 // same bytes when images overlap.  (MODE 0 spans get their CRC from the epoch
 // lanes of k_lines itself.)
-__global__ void k_fix(SpanArgs a, const uint2 *rt, const uint32_t *route) {
+__global__ void k_fix(SpanArgs a, const uint2 *rt, const uint32_t *route, uint32_t xm128) {
     MCRC_VGPR_FLOOR();  // (several workgroups per CU: crc32c_device.h)
     if (route && *route == 0) return;  // (k_lines took no image)
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint2 r = rt[i];
         if (r.y & kRtFused) {
-            const uint32_t crc = ~mulmodp_dev(r.x, a.xpow[kXpowInv + (r.y & 15u)]);
+            const uint32_t crc = ~mulmodp_dev(mulmodp_dev(r.x, xm128), a.xpow[kXpowInv + (r.y & 15u)]);
             uint8_t *p = const_cast<uint8_t *>(a.base) + a.offsets[i] + 32;
             // non-temporal: plain stores left 16 M dirty 32-B sectors in the
             // caches, written back while the next batch streamed (its

@@ -79,7 +79,7 @@ struct Device {
     uint4 *img = nullptr;       // LDS table image of every table kernel (build_lds_image_span, chunk 16)
     uint32_t *tab8 = nullptr;   // byte-wise table (k_count / k_final: a span's head fragment and foreign bytes)
     uint32_t *xpow = nullptr;   // x^(8n) table (layout mcrc_dev::kXpow*)
-    uint32_t *xk = nullptr;     // k_lines: x^(8e), e in [kXkLo, kXkLo + kXkN)
+    uint32_t xm128 = 0;         // k_lines / k_fix: x^(-8 * 128)
     uint4 *zero = nullptr;      // kZeroBytes of zeros (one 4 KiB line set per CU slot)
     unsigned long long *nbad = nullptr;  // [0]: bad / out-of-range count, [1]: walk invariant failures
     unsigned long long *hbad = nullptr;  // pinned twin of nbad[0..1] (a D2H copy into pageable memory is a slow path)
@@ -264,17 +264,7 @@ int init_device(Device &d, int id) {
     HIP_OK(hipMemcpy(d.segpow, sp.data(), sp.size() * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMalloc(&d.xpow, xp.size() * 4));
     HIP_OK(hipMemcpy(d.xpow, xp.data(), xp.size() * 4, hipMemcpyHostToDevice));
-    {
-        std::vector<uint32_t> xk(mcrc_dev::kXkN);
-        const uint32_t up = mcrc::xpow8n(1), down = mcrc::xpow8n_inv(1);  // x^8, x^-8
-        uint32_t v = 0x80000000u;                                          // x^0
-        for (int32_t e = 0; e < (int32_t)mcrc_dev::kXkN + mcrc_dev::kXkLo; ++e, v = mcrc::mulmodp(v, up))
-            xk[e - mcrc_dev::kXkLo] = v;
-        v = 0x80000000u;
-        for (int32_t e = 0; e >= mcrc_dev::kXkLo; --e, v = mcrc::mulmodp(v, down)) xk[e - mcrc_dev::kXkLo] = v;
-        HIP_OK(hipMalloc(&d.xk, xk.size() * 4));
-        HIP_OK(hipMemcpy(d.xk, xk.data(), xk.size() * 4, hipMemcpyHostToDevice));
-    }
+    d.xm128 = mcrc::xpow8n_inv(128);
     HIP_OK(hipMalloc(&d.zero, mcrc_dev::kZeroBytes));
     HIP_OK(hipMemset(d.zero, 0, mcrc_dev::kZeroBytes));
     HIP_OK(hipMalloc(&d.nbad, 2 * sizeof(unsigned long long)));
@@ -460,7 +450,7 @@ template <int MODE, bool OFFS>
 void launch_k5(const Device &d, const mcrc_dev::SpanArgs &a, mcrc_dev::ItemsOut io, hipStream_t st) {
     const int grid = grid_for(d, a.n);
     const uint64_t waves = (uint64_t)grid * (1024 / 64);
-    io.xk = d.xk;
+    io.xm128 = d.xm128;
     io.nsr = (uint32_t)std::min<uint64_t>(mcrc_dev::kEpoch, std::max<uint64_t>(1, (a.n + 2 * waves - 1) / (2 * waves)));
     hipLaunchKernelGGL((mcrc_dev::k_lines<MODE, OFFS>), dim3(grid), dim3(1024), mcrc_dev::kLdsImageK1Bytes, st, a,
                        d.img, io);
@@ -670,7 +660,7 @@ int launch_items(Device &d, mcrc_dev::SpanArgs a, hipStream_t st) {
         HIP_OK(hipEventRecord(d.fork, st));
         HIP_OK(hipStreamWaitEvent(d.side, d.fork, 0));
         hipLaunchKernelGGL(mcrc_dev::k_fix, dim3(g), dim3(256), 0, d.side, a, (const uint2 *)io.rt,
-                           (const uint32_t *)d.route);
+                           (const uint32_t *)d.route, d.xm128);
         HIP_OK(hipEventRecord(d.join, d.side));
         join.armed = true;
     }

@@ -16,6 +16,11 @@ For span D = [p, E) with initial CRC c:
   f the register after D from ~c (the second shift is negative when the
   window runs past B: x^(8e) for e in [-128, 4352) is one table);
 * crc32c(c, D) = ~M_{-pad}(V); a verify is good iff V == M_pad(~stored).
+* Round 6: the epoch lane forms W = M_128(V) = M_d(M_4096(r_h) ^ R) ^
+  M_128(r_t), d = Et - A - 3968 in [0, 272), with the table operators
+  (M_2048 twice, the tree levels M_16..M_128 by the bits of d, byte shifts
+  below 16) instead of two multiplies by x^(8e): a verify is good iff
+  W == M_128(M_pad(~stored)), the CRC is ~M_{-pad-128}(W).
 Checked against the oracle at every 128-B alignment of the fused lengths.
 """
 import numpy as np
@@ -93,8 +98,20 @@ def tail_chain(buf, B, E):
     return chain(dw)
 
 
+def shift_ops(y, d):
+    """M_d(y) for 0 <= d < 512 as finish_run composes it: the tree levels
+    M_256 (M_128 twice), M_128, M_64, M_32, M_16 by the bits of d, then
+    zeros_lds for d mod 16."""
+    assert 0 <= d < 512
+    for bit, n in ((256, 256), (128, 128), (64, 64), (32, 32), (16, 16)):
+        if d & bit:
+            y = zeros(y, n)
+    return zeros(y, d & 15)
+
+
 def kernel_lines(buf, p, length, crc_in=0):
-    """(V, pad) as the line-anchored k_items computes them."""
+    """(V, W, pad) as the line-anchored k_lines computes them (W = M_128(V),
+    round 6's form)."""
     A, B, fused = lines_shape(p, length)
     assert fused
     E = p + length
@@ -108,7 +125,9 @@ def kernel_lines(buf, p, length, crc_in=0):
     window = bytes(buf[A:B]) + bytes(A + BLOCK - B)
     R = raw(window)
     V = mulmodp(r_h, xk(Et - A)) ^ mulmodp(R, xk(Et - A - BLOCK)) ^ r_t
-    return V, pad
+    d = Et - A - (BLOCK - LINE)
+    W = shift_ops(zeros(zeros(r_h, 2048), 2048) ^ R, d) ^ zeros(r_t, 128)
+    return V, W, pad
 
 
 @pytest.mark.parametrize("al", range(0, 128, 5))
@@ -122,15 +141,18 @@ def test_line_anchored_V_is_M_pad_of_the_register(al):
             continue
         D = buf[p:p + length]
         f = reg(M32, D)
-        V, pad = kernel_lines(buf, p, length)
-        assert V == zeros(f, pad)
+        V, W, pad = kernel_lines(buf, p, length)
+        assert V == zeros(f, pad) and W == zeros(V, 128)
         crc = oracle.crc32c(0, D)
         assert ~mulmodp(V, xpow8_inv(pad)) & M32 == crc
-        # verify: good iff V == M_pad(~stored)
+        assert ~mulmodp(mulmodp(W, xpow8_inv(128)), xpow8_inv(pad)) & M32 == crc
+        # verify: good iff V == M_pad(~stored), i.e. W == M_128(M_pad(~stored))
         assert V == zeros(~crc & M32, pad) and V != zeros(~(crc ^ 1) & M32, pad)
+        assert W == zeros(zeros(~crc & M32, pad), 128) and W != zeros(zeros(~(crc ^ 1) & M32, pad), 128)
         c = int(rng.integers(0, 1 << 32))
-        Vc, _ = kernel_lines(buf, p, length, crc_in=c)
+        Vc, Wc, _ = kernel_lines(buf, p, length, crc_in=c)
         assert ~mulmodp(Vc, xpow8_inv(pad)) & M32 == oracle.crc32c(c, D)
+        assert ~mulmodp(mulmodp(Wc, xpow8_inv(128)), xpow8_inv(pad)) & M32 == oracle.crc32c(c, D)
 
 
 def test_line_anchored_shapes():
@@ -145,6 +167,7 @@ def test_line_anchored_shapes():
             E = al + L
             Et = (E + 15) // 16 * 16
             assert 4 <= A - al <= 131 and -128 <= Et - A - BLOCK and Et - A < 4352
+            assert 0 <= Et - A - (BLOCK - LINE) < 272  # (d of finish_run's shift)
     assert not any(lines_shape(al, 4354)[2] and lines_shape(al, 4354)[1] - lines_shape(al, 4354)[0] > BLOCK
                    for al in range(128))
     assert not any(lines_shape(al, L)[2] for L in (3800, 3900, 4500) for al in range(128))
