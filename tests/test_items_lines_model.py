@@ -14,7 +14,8 @@ For span D = [p, E) with initial CRC c:
 * with R = raw of the window from the group's lanes,
     V = M_{Et-A}(r_h) ^ M_{Et-A-4096}(R) ^ r_t = M_pad(f),
   f the register after D from ~c (the second shift is negative when the
-  window runs past B: x^(8e) for e in [-128, 4352) is one table);
+  window runs past B: through round 5 the kernel multiplied by x^(8e) from
+  a table for e in [-128, 4352));
 * crc32c(c, D) = ~M_{-pad}(V); a verify is good iff V == M_pad(~stored).
 * Round 6: the epoch lane forms W = M_128(V) = M_d(M_4096(r_h) ^ R) ^
   M_128(r_t), d = Et - A - 3968 in [0, 272), with the table operators
@@ -46,7 +47,7 @@ def zeros(v, n):
 
 
 def xk(e):
-    """x^(8e) for -128 <= e < 4352 (the kernel's table)."""
+    """x^(8e) for -128 <= e < 4352 (the round-5 kernel's table; V below)."""
     assert -128 <= e < 4352
     return xpow8(e) if e >= 0 else xpow8_inv(-e)
 
