@@ -727,6 +727,43 @@ def test_verify_pages_k5_small_wbufs_walked_twice(torch, wbuf):
     assert nbad == bad.size
 
 
+def test_verify_pages_slot_boundary(torch):
+    """64 KiB wbufs keep 32 walk slots: wbufs of 31, 32 and 33 items (and an
+    empty one and one of a single item), verified as a planned batch (fewer
+    than 4096 items: the emit pass copies the slots of the wbufs that fit
+    and walks the 33-item wbuf again, k_count reads every header): the
+    sequential walk's offsets and the oracle's verdicts, with damaged items
+    on both sides of the boundary."""
+    rng = np.random.default_rng(57)
+    wbuf = 64 << 10
+    parts, offs = [], []
+    for w, n in enumerate([31, 32, 33, 0, 1, 32, 33]):
+        items = [layout.make_item(b"s%02d%05d" % (w, i), rng.integers(0, 256, 1800, dtype=np.uint8).tobytes(),
+                                  cas=w * 100 + i + 1) for i in range(n)]
+        b, o = layout.pack_wbufs(items, wbuf) if items else (np.zeros(wbuf, np.uint8), np.zeros(0, np.uint64))
+        assert b.size == wbuf  # (one wbuf each)
+        parts.append(b)
+        offs.append(o + np.uint64(w * wbuf))
+    buf, offs = np.concatenate(parts), np.concatenate(offs)
+    ok, nbad = mc.stamp_items(buf, offs, region_bytes=wbuf)
+    assert nbad == 0
+    first = np.searchsorted(offs, np.arange(7, dtype=np.uint64) * wbuf)  # each wbuf's first item
+    # the last item of the 31-item wbuf, the first and last (32nd) of the 32-item
+    # one, the first, 32nd and 33rd of the 33-item one, the single item, the last
+    # item of the pages
+    victims = [int(first[1]) - 1, int(first[1]), int(first[2]) - 1, int(first[2]), int(first[2]) + 31,
+               int(first[3]) - 1, int(first[4]), offs.size - 1]
+    for v in victims:
+        buf[int(offs[v]) + 200] ^= 0x10
+    np.testing.assert_array_equal(_walk(buf, wbuf), offs)
+    got_offs, got_ok, nbad = mc.verify_pages(_dev(torch, buf), wbuf)
+    np.testing.assert_array_equal(got_offs.cpu().numpy().astype(np.uint64), offs)
+    expect = np.ones(offs.size, np.uint8)
+    expect[victims] = 0
+    np.testing.assert_array_equal(got_ok.cpu().numpy(), expect)
+    assert nbad == len(victims)
+
+
 def test_chained_iovs(torch):
     """Chunked items (storage.c:163-170): the CRC chained over an item's iovs
     (header from +32, then each chunk) equals crc32c(0, concatenation)."""
