@@ -93,8 +93,15 @@ _RM_NEW = r"""        UnitDesc nd;
         }
         if (last && (lj >> 3) == sl) ring = fetch_unit<UNITS>(a, u + 5 * ustep, ub, lj);"""
 
+# k_spans: a block's first and last 512-B piece rows (lines a span's head or
+# tail block may share with its neighbour span, which the same group takes
+# next in a balanced plan) with the default policy, the rest non-temporal
+_EDGE_OLD = """        w.v[j] = kSpanNT ? ld16_nt(q) : ld16(q);"""
+_EDGE_NEW = """        w.v[j] = kSpanNT && j != 0 && j != (int)kK1Pieces - 1 ? ld16_nt(q) : ld16(q);"""
+
 VARIANTS = {
     "cur": [],
+    "edgecache": [("crc32c_kernels.hip", _EDGE_OLD, _EDGE_NEW)],
     "remat": [("crc32c_kernels.hip", _RM_OLD, _RM_NEW)],
     "u32remat": [("crc32c_kernels.hip", _U32_OLD, _U32_NEW), ("crc32c_kernels.hip", _U32S_OLD, _U32S_NEW),
                  ("crc32c_kernels.hip", _RM_OLD, _RM_NEW)],
